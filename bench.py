@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident MTU-9000 TCP checksum batches (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg5]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one launch of the checksum kernel over this rank's whole shard of
+synthetic packets already resident in HBM (generated on the device from
+global packet ids; cfg5 = 8,980-byte TCP/IPv4 segments, 8M packets per GPU,
+64M at 8 GPUs -> weak scaling).  Ranks share nothing on the data path; gloo
+carries the barrier and the MAX of elapsed times.  Rank 0 prints ONE JSON line.
+
+value   = checksummed L4 bytes of all ranks x K / max-over-ranks wall time, GiB/s
+roofline: algorithmic bytes per launch (L + 2 per packet: L read, u16 written)
+          / mean launch duration from HIP events on the launch stream, vs 8 TB/s
+cpu_baseline: pip's own pip_inet_checksum (oracle/_ref, compiled from the
+          reference) -- or the oracle's C restatement if _ref is absent -- on
+          a bounded sample of the same packets, all host cores; rank 0, N=1.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+from pip_amd import shard  # noqa: E402
+from pip_amd.workloads import ALL, BY_CFG, N_FLOWS  # noqa: E402
+
+METRIC = "GiB/s payload checksummed (device-resident), MTU-9000 TCP batch; Mpkt/s"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PER_GPU_PACKETS = 8 << 20  # cfg5: 64M packets over 8 GPUs
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", default="cfg5", help="cfg2|cfg3|cfg4|cfg5 (default: the headline cfg5)")
+    p.add_argument("--packets-per-gpu", type=int, default=0, help="override the per-GPU shard size")
+    p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")
+    p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and host end-to-end legs")
+    p.add_argument("--traffic", default="", help="JSON file with PMC-measured HBM bytes per launch")
+    return p.parse_args()
+
+
+def host_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap else n)
+
+
+def main() -> int:
+    args = parse()
+    env = shard.dist_env()
+    shard.init_control_plane(env)
+
+    import torch
+
+    from pip_amd import engine
+
+    torch.cuda.set_device(env.local_rank)
+    engine.require_gpu()
+    w = ALL[args.workload] if args.workload in ALL else BY_CFG[int(args.workload.lstrip("cfg"))]
+    per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
+    n_total = per_gpu * env.world
+    first, count = shard.shard_range(n_total, env.world, env.rank)
+
+    # ---- this rank's shard, generated in HBM from global packet ids
+    pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1] if w.family else None
+    if w.ragged:
+        arena, desc, lens = engine.gen_ragged(count, first, w.seed, w.hdr, N_FLOWS)
+        l4_bytes = int(lens.to(torch.int64).sum().item())
+
+        def step(out):
+            return engine.checksum_ragged(arena, desc, pseudo, out=out)
+    else:
+        arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
+        engine.gen_fixed(arena, w.stride, w.length, count, first, w.seed, w.hdr)
+        l4_bytes = count * w.length
+
+        def step(out):
+            return engine.checksum_fixed(arena, w.stride, w.length, count, pseudo, N_FLOWS, None, first, out=out)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step(out)
+    torch.cuda.synchronize()
+    shard.barrier(env)
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step(out)
+    ev1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    shard.barrier(env)
+    elapsed = shard.max_over_ranks(env, t1 - t0)
+    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(args.steps, 1)  # mean launch duration on the launch stream
+    total_bytes = shard.sum_over_ranks(env, float(l4_bytes))
+    total_pkts = shard.sum_over_ranks(env, float(count))
+
+    gib_s = total_bytes * args.steps / elapsed / 2**30
+    mpkt_s = total_pkts * args.steps / elapsed / 1e6
+    algo_bytes = l4_bytes + 2 * count  # per launch on this rank
+    achieved = algo_bytes / launch_s / 1e9
+    traffic = None
+    if args.traffic and Path(args.traffic).exists():
+        traffic = json.loads(Path(args.traffic).read_text()).get("hbm_bytes_per_launch")
+
+    line = {
+        "metric": METRIC,
+        "value": round(gib_s, 2),
+        "unit": "GiB/s",
+        "n_gpus": env.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: device-generated counter-hash packets (0.1% all-zero, 0.1% all-0xFF), 1024 flows",
+        "config": {
+            "workload": f"{w.name}: {w.description}",
+            "packets_per_gpu": count,
+            "global_packets": n_total,
+            "l4_bytes_per_packet": w.length,
+            "arena_stride": w.stride,
+            "parallelism": f"{env.world} shard(s), contiguous packet ranges, no data-path collective",
+        },
+        "mpkt_per_s": round(mpkt_s, 2),
+        "per_gpu_gib_per_s": round(gib_s / env.world, 2),
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel_ms": round(launch_s * 1e3, 4),
+            "algorithmic_bytes_per_launch": algo_bytes,
+        },
+        "cpu_baseline": None,
+    }
+
+    if env.rank == 0 and env.world == 1 and not args.no_cpu and not w.ragged:
+        line["cpu_baseline"], line["host_end_to_end"] = cpu_legs(args, w, out, count, first)
+
+    shard.barrier(env)
+    if env.rank == 0:
+        print(json.dumps(line), flush=True)
+    shard.shutdown(env)
+    return 0
+
+
+def cpu_legs(args, w, gpu_out, count, first):
+    """pip's own checksum on the host cores over a bounded sample of the same
+    packets (checked bit-exact against the GPU results), plus the PCIe-inclusive
+    host -> device -> host rate of the same sample through pipck_host_checksum_fixed."""
+    import ctypes as C
+
+    import numpy as np
+
+    from oracle.oracle import Oracle, Reference
+    from pip_amd import _lib
+
+    threads = host_threads()
+    n = args.cpu_sample or min(count, max(1, (2 << 30) // w.stride))  # ~2 GiB sample
+    orc = Oracle()
+    lib = _lib.load()
+    pin = lib.pipck_host_alloc(n * w.stride)
+    if not pin:
+        raise RuntimeError("pipck_host_alloc failed")
+    arena = np.ctypeslib.as_array((C.c_uint8 * (n * w.stride)).from_address(pin))
+    try:
+        orc.lib.ock_gen_fixed_batch(w.seed, first, n, w.length, w.hdr, C.c_void_p(pin), w.stride, threads)
+        flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto) if w.family else b""
+        if Reference.available():
+            ref, kind = Reference(), "reference"
+
+            def run(t):
+                return ref.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, flows, N_FLOWS, first, t)
+        else:
+            kind = "port"
+
+            def run(t):
+                return orc.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, w.seed, N_FLOWS, first, t)
+
+        res = run(threads)  # warm + correctness
+        gpu = gpu_out[:n].cpu().numpy().view(np.uint16)
+        verified = bool(np.array_equal(res, gpu))
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            run(threads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el > 3.0 or reps >= 50:
+                break
+        mt = n * w.length * reps / el / 2**30
+        t0 = time.perf_counter()
+        run(1)
+        st = n * w.length / (time.perf_counter() - t0) / 2**30
+
+        # host end-to-end: pinned host batch -> H2D -> kernel -> D2H (PCIe-bound)
+        ctx = C.c_void_p()
+        _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+        h_out = np.zeros(n, dtype=np.uint16)
+        fl = C.create_string_buffer(flows, max(len(flows), 1))
+        call = lambda: lib.pipck_host_checksum_fixed(  # noqa: E731
+            ctx, C.c_void_p(pin), w.stride, w.length, n, w.family, fl, N_FLOWS, first, C.c_void_p(h_out.ctypes.data))
+        _lib.check("pipck_host_checksum_fixed", call())
+        t0 = time.perf_counter()
+        for _ in range(3):
+            call()
+        e2e = n * w.length * 3 / (time.perf_counter() - t0) / 2**30
+        e2e_ok = bool(np.array_equal(h_out, res))
+        lib.pipck_ctx_destroy(ctx)
+    finally:
+        del arena
+        lib.pipck_host_free(pin)
+    cpu = {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+           "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.2f} GiB), "
+                     f"{reps} timed passes on {threads} threads; 1 thread: {st:.3f} GiB/s",
+           "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified}
+    e2e_d = {"value": round(e2e, 2), "unit": "GiB/s", "sample_packets": n, "pinned": True, "results_match": e2e_ok}
+    return cpu, e2e_d
+
+
+if __name__ == "__main__":
+    sys.exit(main())

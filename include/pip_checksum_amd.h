@@ -1,0 +1,42 @@
+// pip_checksum_amd.h -- the C++ drop-in for plumk97/pip's checksum API,
+// exported by libpip_checksum_amd.so with the reference's exact signatures and
+// therefore its exact mangled names:
+//
+//   _Z15pip_fold_uint32j                                  pip/pip_checksum.cpp:9   (exported, undeclared)
+//   _Z21pip_standard_checksumPKvjj                        pip/pip_checksum.h:17
+//   _Z15pip_ip_checksumPKvj                               pip/pip_checksum.h:22
+//   _Z17pip_inet_checksumPKvh7in_addrS1_t                 pip/pip_checksum.h:30
+//   _Z18pip_inet6_checksumPKvh8in6_addrS1_t               pip/pip_checksum.h:31
+//   _Z21pip_inet_checksum_bufSt10shared_ptrI7pip_bufEh7in_addrS2_   pip/pip_checksum.h:33
+//   _Z22pip_inet6_checksum_bufSt10shared_ptrI7pip_bufEh8in6_addrS2_ pip/pip_checksum.h:34
+//
+// pip's callers (pip/pip_netif.cpp:97, pip/protocol/pip_udp.cpp:50,60,
+// pip/protocol/pip_tcp_packet.cpp:128,130) keep including pip's own
+// pip_checksum.h; a build links this library instead of pip_checksum.cpp
+// (INTEGRATION.md).  This header exists for users outside pip's tree.
+//
+// Every call computes on the MI355X through the C ABI in pipck.h
+// (pipck_host_sum); there is no CPU compute path.  A missing or failing GPU
+// is fatal: the message is printed and the process aborts, because pip's API
+// has no error channel (pip_checksum.h returns bare integers).
+#ifndef PIP_CHECKSUM_AMD_H
+#define PIP_CHECKSUM_AMD_H
+
+#include <netinet/in.h>
+#include <stdint.h>
+
+#include <memory>
+
+class pip_buf;  // pip/pip_buf.h:13 -- only read through its layout (pip_buf_layout.h)
+
+uint32_t pip_fold_uint32(uint32_t num);
+uint32_t pip_standard_checksum(const void* payload, uint32_t len, uint32_t sum);
+uint16_t pip_ip_checksum(const void* payload, uint32_t len);
+uint16_t pip_inet_checksum(const void* payload, uint8_t proto, struct in_addr src, struct in_addr dst, uint16_t len);
+uint16_t pip_inet6_checksum(const void* payload, uint8_t proto, struct in6_addr src, struct in6_addr dst,
+                            uint16_t len);
+uint16_t pip_inet_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src, struct in_addr dst);
+uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
+                                struct in6_addr dst);
+
+#endif

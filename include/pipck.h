@@ -1,0 +1,174 @@
+/*
+ * pipck.h -- C ABI of the MI355X Internet-checksum engine (libpipck.so).
+ *
+ * The engine computes plumk97/pip's one's-complement checksum
+ * (pip/pip_checksum.cpp) on AMD MI355X (gfx950) with hand-written HIP kernels.
+ * Everything here is plain C: pointers, sizes, int status codes; no torch or
+ * C++ types.  Two layers:
+ *
+ *   1. Batch ABI (device-resident, the performance path).  Packets already in
+ *      HBM, results (host-order u16, exactly what pip returns before the
+ *      caller's htons) written to HBM.  Stream-ordered, asynchronous.
+ *   2. Host ABI (context-owned buffers).  Host batches are pipelined
+ *      H2D -> kernel -> D2H on two HIP streams; single packets / pip_buf chains
+ *      go through an exact-semantics kernel.  libpip_checksum_amd.so (the C++
+ *      drop-in for pip's six functions, include/pip_checksum_amd.h) is built on
+ *      this layer.
+ *
+ * Reference interface each entry point replaces is cited per declaration.
+ * Result semantics are bit-exact with pip_checksum.cpp, including 0x0000 being
+ * returned as-is (never mapped to 0xFFFF) and per-segment odd-byte padding of
+ * chains (pip_checksum.cpp:110-112, :145-147).
+ *
+ * Domain of the batch ABI: every segment is at most 65535 bytes (the IPv4/IPv6
+ * payload-length field).  In that domain pip's u32 accumulator can never wrap,
+ * which lets the kernels sum in any order.  The host ABI has no length limit
+ * and reproduces pip's mod-2^32 wrap exactly (pip_checksum.cpp:16-23).
+ */
+#ifndef PIPCK_H
+#define PIPCK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define PIPCK_OK         0
+#define PIPCK_EINVAL     1   /* bad argument (null pointer, zero flows, ...) */
+#define PIPCK_ERANGE     2   /* a segment longer than 65535 bytes in a batch */
+#define PIPCK_EHIP       3   /* a HIP runtime call failed; see pipck_last_error() */
+#define PIPCK_ENODEV     4   /* no gfx950 device / HIP unavailable */
+#define PIPCK_ENOMEM     5
+
+#define PIPCK_MAX_SEG_LEN 65535u
+
+/* Human-readable text of the last error on the calling thread. */
+const char* pipck_last_error(void);
+/* ABI version, (major << 16) | minor. */
+uint32_t pipck_version(void);
+
+/* ---- flows / pseudo-headers ------------------------------------------ */
+/* One flow = one (src, dst, proto) pseudo-header; packet i of a batch uses
+ * flow  flow_of ? flow_of[i] : (flow_origin + i) % n_flows.
+ * Addresses are in network order exactly as in struct in_addr / in6_addr.  */
+typedef struct pipck_flow4 {
+    uint32_t src;      /* in_addr.s_addr */
+    uint32_t dst;
+    uint8_t  proto;    /* IPPROTO_TCP / IPPROTO_UDP / ... */
+    uint8_t  pad[3];
+} pipck_flow4;
+
+typedef struct pipck_flow6 {
+    uint8_t src[16];   /* in6_addr */
+    uint8_t dst[16];
+    uint8_t proto;
+    uint8_t pad[3];
+} pipck_flow6;
+
+/* Reduce a device flow table to one u32 pseudo-header base per flow:
+ * src hi+lo + dst hi+lo + proto (pip_checksum.cpp:46-55 for v4, :70-82 for v6).
+ * The per-packet length term is added by the checksum kernels. */
+int pipck_flows4_prepare(const pipck_flow4* d_flows, uint32_t n_flows, uint32_t* d_pseudo, void* stream);
+int pipck_flows6_prepare(const pipck_flow6* d_flows, uint32_t n_flows, uint32_t* d_pseudo, void* stream);
+
+/* ---- batch ABI (device pointers, stream-ordered) ----------------------- */
+/* d_pseudo == NULL selects pip_ip_checksum semantics (no pseudo-header,
+ * pip_checksum.cpp:35-39).  Otherwise the result is
+ *   ~fold(pseudo[flow] + hi16(len) + lo16(len) + sum16be(bytes))
+ * which equals pip_inet_checksum / pip_inet6_checksum (pip_checksum.cpp:42-87)
+ * and pip_inet{,6}_checksum_buf on a single-segment chain (:90-148).        */
+
+/* Fixed stride: packet i = d_arena + i*stride, len bytes.  Any alignment. */
+int pipck_checksum_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
+                         const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                         uint64_t flow_origin, uint16_t* d_out, void* stream);
+
+/* Ragged: one descriptor per packet. */
+typedef struct pipck_desc {
+    uint64_t offset;   /* byte offset of the packet (or segment) in the arena; any alignment */
+    uint32_t len;      /* bytes, <= 65535 */
+    uint32_t flow;     /* flow index (ignored when d_pseudo == NULL and for chain segments) */
+} pipck_desc;
+
+/* d_err (optional, device u32): OR-ed with (1 << PIPCK_ERANGE) when a
+ * descriptor is out of domain; that packet's result is then 0. */
+int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
+                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_err, void* stream);
+
+/* Chains (pip_buf lists, pip_checksum.cpp:90-148): packet p owns segments
+ * [d_seg_begin[p], d_seg_begin[p+1]); its pseudo-header length term is the
+ * u32 sum of its segment lengths (pip_buf::total_len).  Every segment is
+ * summed from its own start, exactly like pip's per-segment loop.
+ * d_scratch: device u32[n_segs]. */
+int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs,
+                          const uint64_t* d_seg_begin, const uint32_t* d_pkt_flow, uint64_t n_packets,
+                          const uint32_t* d_pseudo, uint32_t* d_scratch, uint16_t* d_out, uint32_t* d_err,
+                          void* stream);
+
+/* RX verification (a capability pip lacks): same
+ * inputs as pipck_checksum_fixed but the packets carry their checksum field;
+ * d_ok[i] = 1 when the one's-complement sum including the pseudo-header is
+ * 0xFFFF (a valid packet), else 0. */
+int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
+                       const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                       uint64_t flow_origin, uint8_t* d_ok, void* stream);
+
+/* Launch-shape override for tuning (0 = automatic).  lanes_per_packet in
+ * {1,2,4,8,16,32,64}; blocks = grid size cap. */
+void pipck_tune(uint32_t lanes_per_packet, uint32_t blocks);
+
+/* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */
+#define PIPCK_HDR_NONE 0
+#define PIPCK_HDR_TCP  1
+#define PIPCK_HDR_UDP  2
+#define PIPCK_HDR_IPV4 3
+uint64_t pipck_cfg_seed(uint32_t cfg);
+/* packets [first_pkt, first_pkt+n) at d_arena + i*stride; bytes [len,stride) zeroed */
+int pipck_gen_fixed(void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint64_t first_pkt,
+                    uint64_t seed, uint32_t hdr_kind, void* stream);
+/* Zipf lengths 64..9000 for packets [first_pkt, first_pkt+n) -> d_len */
+int pipck_gen_zipf_lengths(uint32_t* d_len, uint64_t n, uint64_t first_pkt, uint64_t seed, void* stream);
+/* descriptors: offsets = exclusive prefix of roundup16(len); flow = (first_pkt+i) % n_flows.
+ * *arena_bytes receives the arena size needed (synchronises the stream). */
+int pipck_gen_ragged_layout(const uint32_t* d_len, uint64_t n, uint64_t first_pkt, uint32_t n_flows,
+                            pipck_desc* d_desc, uint64_t* arena_bytes, void* stream);
+int pipck_gen_ragged_fill(void* d_arena, const pipck_desc* d_desc, uint64_t n, uint64_t first_pkt,
+                          uint64_t seed, uint32_t hdr_kind, void* stream);
+int pipck_gen_flows4(pipck_flow4* d_flows, uint32_t n_flows, uint64_t seed, uint8_t proto, void* stream);
+int pipck_gen_flows6(pipck_flow6* d_flows, uint32_t n_flows, uint64_t seed, uint8_t proto, void* stream);
+
+/* ---- host ABI ---------------------------------------------------------- */
+typedef struct pipck_ctx pipck_ctx;
+
+/* device < 0 selects the current HIP device. */
+int pipck_ctx_create(int device, pipck_ctx** out);
+int pipck_ctx_destroy(pipck_ctx* ctx);
+
+/* One segment of a host-memory packet/chain. */
+typedef struct pipck_hseg {
+    const void* ptr;
+    uint32_t len;
+} pipck_hseg;
+
+/* pip's exact sequential semantics over host bytes, computed on the device:
+ *   sum = init; for each seg: sum = fold(fold((sum + sum16be(seg)) mod 2^32))
+ * (pip_standard_checksum, pip_checksum.cpp:13-33, chained as at :110-112).
+ * *out receives the final folded u32 in [0, 0xFFFF].  Synchronous. */
+int pipck_host_sum(pipck_ctx* ctx, const pipck_hseg* segs, uint32_t nseg, uint32_t init, uint32_t* out);
+
+/* Host-resident fixed-stride batch: H2D in chunks, kernel, D2H of results,
+ * double-buffered over two streams.  h_arena may be pageable or pinned
+ * (pinned: see pipck_host_alloc).  Flows are host tables (v4 or v6, by family). */
+int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stride, uint32_t len,
+                              uint64_t n_packets, int family, const void* h_flows, uint32_t n_flows,
+                              uint64_t flow_origin, uint16_t* h_out);
+void* pipck_host_alloc(size_t bytes);   /* pinned host memory */
+void  pipck_host_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIPCK_H */

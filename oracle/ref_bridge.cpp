@@ -1,0 +1,100 @@
+// ref_bridge.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// extern "C" entry points over the REAL reference functions of
+// /root/reference/pip/pip_checksum.cpp, so Python tests (ctypes) and the
+// bench's cpu_baseline leg can call pip's own code.  Compiled against the
+// reference's headers where they lie (oracle/Makefile, target `ref`); the
+// output goes to oracle/_ref/ only.  Nothing from the reference is copied
+// into this repository.
+#include "pip_checksum.h"
+
+#include <cstring>
+#include <thread>
+#include <vector>
+
+// Exported by pip_checksum.cpp:9 but not declared in its header.
+pip_uint32 pip_fold_uint32(pip_uint32 num);
+
+extern "C" {
+
+uint32_t ref_fold_uint32(uint32_t x) { return pip_fold_uint32(x); }
+
+uint32_t ref_standard_checksum(const void* p, uint32_t len, uint32_t sum) {
+    return pip_standard_checksum(p, len, sum);
+}
+
+uint16_t ref_ip_checksum(const void* p, uint32_t len) { return pip_ip_checksum(p, len); }
+
+uint16_t ref_inet_checksum(const void* p, uint8_t proto, uint32_t src, uint32_t dst, uint16_t len) {
+    pip_in_addr s, d;
+    s.s_addr = src;
+    d.s_addr = dst;
+    return pip_inet_checksum(p, proto, s, d, len);
+}
+
+uint16_t ref_inet6_checksum(const void* p, uint8_t proto, const uint8_t* src, const uint8_t* dst,
+                            uint16_t len) {
+    pip_in6_addr s, d;
+    std::memcpy(&s, src, 16);
+    std::memcpy(&d, dst, 16);
+    return pip_inet6_checksum(p, proto, s, d, len);
+}
+
+static std::shared_ptr<pip_buf> make_chain(const void* const* segs, const uint32_t* lens, uint32_t nseg) {
+    std::shared_ptr<pip_buf> head, tail;
+    std::vector<std::shared_ptr<pip_buf>> all;
+    for (uint32_t i = 0; i < nseg; i++) all.push_back(std::make_shared<pip_buf>(segs[i], lens[i], 0));
+    // link back to front so total_len propagates the way pip builds chains
+    for (int i = (int)nseg - 2; i >= 0; i--) all[i]->set_next(all[i + 1]);
+    return nseg ? all[0] : std::make_shared<pip_buf>(nullptr, 0, 0);
+}
+
+uint16_t ref_inet_checksum_chain(const void* const* segs, const uint32_t* lens, uint32_t nseg, uint8_t proto,
+                                 uint32_t src, uint32_t dst) {
+    pip_in_addr s, d;
+    s.s_addr = src;
+    d.s_addr = dst;
+    return pip_inet_checksum_buf(make_chain(segs, lens, nseg), proto, s, d);
+}
+
+uint16_t ref_inet6_checksum_chain(const void* const* segs, const uint32_t* lens, uint32_t nseg, uint8_t proto,
+                                  const uint8_t* src, const uint8_t* dst) {
+    pip_in6_addr s, d;
+    std::memcpy(&s, src, 16);
+    std::memcpy(&d, dst, 16);
+    return pip_inet6_checksum_buf(make_chain(segs, lens, nseg), proto, s, d);
+}
+
+// CPU baseline: pip's own pip_inet{,6}_checksum / pip_ip_checksum over a
+// fixed-stride batch, on `threads` std::threads with contiguous shards.
+// flows4: n_flows x {src s_addr, dst s_addr}; flows6: n_flows x 32 bytes.
+void ref_batch_fixed(const uint8_t* arena, uint64_t stride, uint32_t len, uint64_t n, int family, uint8_t proto,
+                     const uint32_t* flows4, const uint8_t* flows6, uint32_t n_flows, uint64_t flow_origin,
+                     uint16_t* out, int threads) {
+    if (threads < 1) threads = 1;
+    auto work = [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            const uint8_t* p = arena + i * stride;
+            uint32_t f = (uint32_t)((flow_origin + i) % n_flows);
+            if (family == 4) {
+                pip_in_addr s, d;
+                s.s_addr = flows4[2 * f];
+                d.s_addr = flows4[2 * f + 1];
+                out[i] = pip_inet_checksum(p, proto, s, d, (pip_uint16)len);
+            } else if (family == 6) {
+                pip_in6_addr s, d;
+                std::memcpy(&s, flows6 + 32 * f, 16);
+                std::memcpy(&d, flows6 + 32 * f + 16, 16);
+                out[i] = pip_inet6_checksum(p, proto, s, d, (pip_uint16)len);
+            } else {
+                out[i] = pip_ip_checksum(p, len);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, n * t / threads, n * (t + 1) / threads);
+    work(0, n / threads);
+    for (auto& x : th) x.join();
+}
+
+}  // extern "C"

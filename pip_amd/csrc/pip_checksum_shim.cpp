@@ -1,0 +1,117 @@
+// pip_checksum_shim.cpp -- libpip_checksum_amd.so: pip's six checksum
+// functions (pip/pip_checksum.h:17-34, plus pip_fold_uint32 at
+// pip/pip_checksum.cpp:9) with identical signatures, computed on the MI355X.
+//
+// Each call marshals its pseudo-header terms (pip_checksum.cpp:46-55, 70-82,
+// 130-142, 161-176) into the initial sum and hands the payload bytes -- one
+// segment, or every segment of a pip_buf chain in order -- to
+// pipck_host_sum(), which replays pip's per-segment loop on the device.
+// Contexts are per thread (thread_local), so calls stay reentrant and
+// lock-free across pip's TX threads, as pip's own functions are.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "../../include/pip_buf_layout.h"
+#include "../../include/pip_checksum_amd.h"
+#include "../../include/pipck.h"
+
+namespace {
+
+[[noreturn]] void die(const char* what, int rc) {
+    std::fprintf(stderr, "libpip_checksum_amd: %s failed (status %d): %s\n", what, rc, pipck_last_error());
+    std::abort();
+}
+
+struct ThreadCtx {
+    pipck_ctx* ctx = nullptr;
+    ~ThreadCtx() {
+        if (ctx) pipck_ctx_destroy(ctx);
+    }
+    pipck_ctx* get() {
+        if (!ctx) {
+            int rc = pipck_ctx_create(-1, &ctx);
+            if (rc) die("pipck_ctx_create", rc);
+        }
+        return ctx;
+    }
+};
+thread_local ThreadCtx t_ctx;
+
+uint32_t device_sum(const pipck_hseg* segs, uint32_t nseg, uint32_t init) {
+    uint32_t out = 0;
+    int rc = pipck_host_sum(t_ctx.get(), segs, nseg, init, &out);
+    if (rc) die("pipck_host_sum", rc);
+    return out;
+}
+
+// ntohl() of an address word as stored in memory
+uint32_t be32(const void* p) {
+    const uint8_t* b = (const uint8_t*)p;
+    return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+}
+uint32_t split(uint32_t a) { return (a >> 16) + (a & 0xFFFFu); }
+uint32_t v4_terms(const in_addr& a) { return split(be32(&a.s_addr)); }
+uint32_t v6_terms(const in6_addr& a) {
+    uint32_t s = 0;
+    for (int i = 0; i < 4; i++) s += split(be32(a.s6_addr + 4 * i));
+    return s;
+}
+
+// Collect a chain's segments in order (pip_checksum.cpp:145).
+uint16_t chain_checksum(const std::shared_ptr<pip_buf>& buf, uint32_t pseudo) {
+    const pip_buf_layout* head = reinterpret_cast<const pip_buf_layout*>(buf.get());
+    pipck_hseg local[8];
+    pipck_hseg* segs = local;
+    uint32_t n = 0, cap = 8;
+    for (const pip_buf_layout* q = head; q; q = q->next) {
+        if (n == cap) {
+            pipck_hseg* bigger = (pipck_hseg*)std::malloc(sizeof(pipck_hseg) * cap * 2);
+            if (!bigger) die("malloc", PIPCK_ENOMEM);
+            std::memcpy(bigger, segs, sizeof(pipck_hseg) * n);
+            if (segs != local) std::free(segs);
+            segs = bigger;
+            cap *= 2;
+        }
+        segs[n++] = pipck_hseg{q->payload, q->payload_len};
+    }
+    // length term: the head's u32 total_len split hi + lo (pip_checksum.cpp:140-142)
+    const uint32_t total = head->total_len;
+    const uint32_t sum = device_sum(segs, n, pseudo + split(total));
+    if (segs != local) std::free(segs);
+    return (uint16_t)~(uint16_t)sum;
+}
+
+}  // namespace
+
+uint32_t pip_fold_uint32(uint32_t num) { return (num & 0x0000FFFFu) + (num >> 16); }
+
+uint32_t pip_standard_checksum(const void* payload, uint32_t len, uint32_t sum) {
+    pipck_hseg s{payload, len};
+    return device_sum(&s, 1, sum);
+}
+
+uint16_t pip_ip_checksum(const void* payload, uint32_t len) {
+    return (uint16_t)~(uint16_t)pip_standard_checksum(payload, len, 0);
+}
+
+uint16_t pip_inet_checksum(const void* payload, uint8_t proto, struct in_addr src, struct in_addr dst,
+                           uint16_t len) {
+    const uint32_t pseudo = v4_terms(src) + v4_terms(dst) + proto + len;
+    return (uint16_t)~(uint16_t)pip_standard_checksum(payload, len, pseudo);
+}
+
+uint16_t pip_inet6_checksum(const void* payload, uint8_t proto, struct in6_addr src, struct in6_addr dst,
+                            uint16_t len) {
+    const uint32_t pseudo = v6_terms(src) + v6_terms(dst) + proto + len;
+    return (uint16_t)~(uint16_t)pip_standard_checksum(payload, len, pseudo);
+}
+
+uint16_t pip_inet_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src, struct in_addr dst) {
+    return chain_checksum(buf, v4_terms(src) + v4_terms(dst) + proto);
+}
+
+uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
+                                struct in6_addr dst) {
+    return chain_checksum(buf, v6_terms(src) + v6_terms(dst) + proto);
+}

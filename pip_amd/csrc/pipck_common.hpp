@@ -1,0 +1,38 @@
+// pipck_common.hpp -- host-side plumbing shared by the libpipck.so sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/pipck.h"
+
+namespace pipck {
+
+void set_error(const std::string& msg);
+
+// Map a HIP failure to PIPCK_EHIP with a message naming the call site.
+inline int hip_fail(hipError_t e, const char* what) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return PIPCK_EHIP;
+}
+
+#define PIPCK_HIP(call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return ::pipck::hip_fail(e_, #call); \
+    } while (0)
+
+// After a kernel launch: report launch-configuration errors synchronously.
+#define PIPCK_LAUNCHED(name)                              \
+    do {                                                  \
+        hipError_t e_ = hipGetLastError();                \
+        if (e_ != hipSuccess) return ::pipck::hip_fail(e_, name); \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Number of CUs on the current device (cached per device).
+int device_cus();
+
+}  // namespace pipck

@@ -1,0 +1,78 @@
+// pipck_device.hpp -- device-side arithmetic of the checksum engine (gfx950).
+//
+// Why order-free summation is exact.  pip (pip/pip_checksum.cpp:13-33) adds
+// big-endian 16-bit words into a u32 and folds twice.  For a segment of at most
+// 65535 bytes plus any pseudo-header, that u32 cannot wrap, and for a total T
+// that did not wrap, fold(fold(T)) is
+//     0                        if T == 0
+//     1 + (T - 1) mod 0xFFFF   otherwise,
+// i.e. it depends only on T mod 0xFFFF and on whether T == 0.  Both are
+// preserved by every reduction used below:
+//   * 2^16 == 1 (mod 0xFFFF), so a little-endian u32 word w contributes
+//     w mod 0xFFFF == lo16(w) + hi16(w), and a u64 sum of LE u32 words has the
+//     residue of the LE 16-bit word sum;
+//   * the big-endian sum of a segment is 256 x its LE sum (mod 0xFFFF) when the
+//     segment starts at an even address, and equal to it when it starts at an
+//     odd one (pip restarts byte pairing at every chain segment,
+//     pip_checksum.cpp:110-112) -- multiplying by 256 mod 0xFFFF is a 16-bit
+//     byte swap;
+//   * every fold used here maps 0 -> 0 and nonzero -> nonzero.
+// So the kernels load 16-byte chunks at aligned addresses, sum LE dwords in any
+// order, and only fix byte order once per segment.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pipck {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// residue- and zero-preserving folds
+__device__ __forceinline__ uint32_t fold64(uint64_t x) {
+    return (uint32_t)(x & 0xFFFFu) + (uint32_t)((x >> 16) & 0xFFFFu) + (uint32_t)((x >> 32) & 0xFFFFu) +
+           (uint32_t)(x >> 48);
+}
+__device__ __forceinline__ uint32_t fold32(uint32_t x) { return (x & 0xFFFFu) + (x >> 16); }
+// pip_fold_uint32 applied twice (pip_checksum.cpp:29-30); result in [0, 0xFFFF]
+__device__ __forceinline__ uint32_t fold16(uint32_t x) { return fold32(fold32(x)); }
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
+
+// Keep bytes [lo, hi) of a 16-byte chunk (0 <= lo, hi <= 16).
+__device__ __forceinline__ uint32_t byte_window(int lo, int hi, int k) {
+    int a = min(max(lo - 4 * k, 0), 4), b = min(max(hi - 4 * k, 0), 4);
+    uint32_t mb = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    uint32_t ma = a >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a)) - 1u);
+    return mb & ~ma;
+}
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi) {
+    v.x &= byte_window(lo, hi, 0);
+    v.y &= byte_window(lo, hi, 1);
+    v.z &= byte_window(lo, hi, 2);
+    v.w &= byte_window(lo, hi, 3);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t sum4(u32x4 v) {
+    return (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
+}
+
+// LE residue sum of a segment -> pip's big-endian folded segment sum in [0,0xFFFF]
+__device__ __forceinline__ uint32_t be_fold(uint32_t le_residue_sum, uintptr_t seg_addr) {
+    uint32_t w = fold16(le_residue_sum);
+    return (seg_addr & 1) ? w : bswap16(w);
+}
+
+// pseudo-header length term: pip adds total_len hi + lo (pip_checksum.cpp:140-142);
+// identical to the flat variants' (u16)len (:91) inside the batch domain.
+__device__ __forceinline__ uint32_t len_term(uint32_t len) { return (len >> 16) + (len & 0xFFFFu); }
+
+// ~(u16)fold(fold(P + F)) -- pip_checksum.cpp:95/:121/:149/:182
+__device__ __forceinline__ uint16_t finish(uint32_t pseudo_total, uint32_t be_sum) {
+    return (uint16_t)~fold16(pseudo_total + be_sum);
+}
+
+// Non-temporal 16-byte load: the arena is streamed exactly once.
+__device__ __forceinline__ u32x4 load_stream(const u32x4* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ u32x4 load_plain(const u32x4* p) { return *p; }
+
+}  // namespace pipck

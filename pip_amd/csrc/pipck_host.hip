@@ -1,0 +1,320 @@
+// pipck_host.hip -- host ABI of the engine: contexts, host-memory batches and
+// pip's exact per-packet semantics on the device.
+//
+// pipck_host_sum() is what the C++ drop-in (pip_checksum_shim.cpp) calls for
+// each of pip's six functions.  Unlike the batch kernels it has no length
+// limit, so it reproduces pip's u32 accumulator exactly, wrap included
+// (pip/pip_checksum.cpp:16-23): the device computes, per segment, the exact
+// sums A (bytes at even offsets) and B (bytes at odd offsets) in u64, and the
+// big-endian word sum of the segment is 256*A + B; one thread then replays
+// pip's chain loop  sum = fold(fold(sum + 256*A + B mod 2^32))  (:110-112).
+#include "pipck_common.hpp"
+#include "pipck_device.hpp"
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace pipck {
+
+static thread_local std::string t_err;
+void set_error(const std::string& msg) { t_err = msg; }
+
+int device_cus() {
+    static std::mutex mu;
+    static std::vector<int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::lock_guard<std::mutex> g(mu);
+    if ((size_t)dev >= cache.size()) cache.resize(dev + 1, 0);
+    if (!cache[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        cache[dev] = cus;
+    }
+    return cache[dev];
+}
+
+// ---------------------------------------------------------------------------
+// exact chain kernel: one 1024-thread block walks the segments in order
+// ---------------------------------------------------------------------------
+struct SegRef {
+    uint64_t offset;  // 16-byte aligned offset in the staging buffer
+    uint32_t len;
+    uint32_t pad;
+};
+
+__global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict__ stage, const SegRef* __restrict__ segs,
+                                                      uint32_t nseg, uint32_t init, uint32_t* __restrict__ out) {
+    __shared__ uint64_t sa[16], sb[16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t sum = init;  // meaningful in thread 0 only
+    for (uint32_t s = 0; s < nseg; s++) {
+        const SegRef r = segs[s];
+        const u32x4* base = reinterpret_cast<const u32x4*>(stage + r.offset);
+        const uint32_t nch = (r.len + 15) / 16;
+        uint64_t A = 0, B = 0;
+        for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
+            u32x4 v = base[c];
+            const int hi = (int)r.len - 16 * (int)c;
+            if (hi < 16) v = mask_chunk(v, 0, hi);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {  // offsets within the segment: 4k+0, 4k+2 even; 4k+1, 4k+3 odd
+                const uint32_t x = v[k];
+                A += (x & 0xFFu) + ((x >> 16) & 0xFFu);
+                B += ((x >> 8) & 0xFFu) + (x >> 24);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            A += __shfl_xor(A, off, 64);
+            B += __shfl_xor(B, off, 64);
+        }
+        if (lane == 0) {
+            sa[w] = A;
+            sb[w] = B;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t tA = 0, tB = 0;
+            for (int i = 0; i < nw; i++) {
+                tA += sa[i];
+                tB += sb[i];
+            }
+            sum += (uint32_t)(256ull * tA + tB);  // u32 wrap exactly as pip's accumulator
+            sum = fold16(sum);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sum;
+}
+
+}  // namespace pipck
+
+using namespace pipck;
+
+struct pipck_ctx {
+    int device = 0;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    // exact path staging
+    uint8_t* h_stage = nullptr;  // pinned
+    uint8_t* d_stage = nullptr;
+    size_t stage_cap = 0;
+    uint32_t* d_result = nullptr;
+    uint32_t* h_result = nullptr;  // pinned
+    // host batch pipeline
+    uint8_t* d_chunk[2] = {nullptr, nullptr};
+    uint16_t* d_out[2] = {nullptr, nullptr};
+    size_t chunk_cap = 0;
+    uint32_t* d_pseudo = nullptr;
+    void* d_flows = nullptr;
+    uint32_t flows_cap = 0;
+    std::mutex mu;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int grow_stage(pipck_ctx* c, size_t need) {
+    if (need <= c->stage_cap) return PIPCK_OK;
+    size_t cap = need < (1u << 20) ? (1u << 20) : need + need / 2;
+    if (c->h_stage) PIPCK_HIP(hipHostFree(c->h_stage));
+    if (c->d_stage) PIPCK_HIP(hipFree(c->d_stage));
+    c->h_stage = nullptr;
+    c->d_stage = nullptr;
+    c->stage_cap = 0;
+    PIPCK_HIP(hipHostMalloc((void**)&c->h_stage, cap, hipHostMallocDefault));
+    PIPCK_HIP(hipMalloc((void**)&c->d_stage, cap));
+    c->stage_cap = cap;
+    return PIPCK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pipck_last_error(void) { return pipck::t_err.c_str(); }
+
+int pipck_ctx_create(int device, pipck_ctx** out) {
+    if (!out) return PIPCK_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0) {
+        set_error(std::string("pipck_ctx_create: no HIP device: ") + hipGetErrorString(e));
+        return PIPCK_ENODEV;
+    }
+    if (device < 0) PIPCK_HIP(hipGetDevice(&device));
+    if (device >= n) {
+        set_error("pipck_ctx_create: device index out of range");
+        return PIPCK_EINVAL;
+    }
+    DeviceGuard g(device);
+    hipDeviceProp_t prop;
+    PIPCK_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error(std::string("pipck_ctx_create: device is ") + prop.gcnArchName + ", libpipck is built for gfx950");
+        return PIPCK_ENODEV;
+    }
+    pipck_ctx* c = new pipck_ctx();
+    c->device = device;
+    for (int i = 0; i < 2; i++) {
+        PIPCK_HIP(hipStreamCreateWithFlags(&c->stream[i], hipStreamNonBlocking));
+        PIPCK_HIP(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
+    }
+    PIPCK_HIP(hipMalloc((void**)&c->d_result, sizeof(uint32_t)));
+    PIPCK_HIP(hipHostMalloc((void**)&c->h_result, sizeof(uint32_t), hipHostMallocDefault));
+    *out = c;
+    return PIPCK_OK;
+}
+
+int pipck_ctx_destroy(pipck_ctx* c) {
+    if (!c) return PIPCK_OK;
+    DeviceGuard g(c->device);
+    for (int i = 0; i < 2; i++) {
+        if (c->stream[i]) (void)hipStreamSynchronize(c->stream[i]);
+        if (c->d_chunk[i]) (void)hipFree(c->d_chunk[i]);
+        if (c->d_out[i]) (void)hipFree(c->d_out[i]);
+        if (c->done[i]) (void)hipEventDestroy(c->done[i]);
+        if (c->stream[i]) (void)hipStreamDestroy(c->stream[i]);
+    }
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->d_stage) (void)hipFree(c->d_stage);
+    if (c->d_result) (void)hipFree(c->d_result);
+    if (c->h_result) (void)hipHostFree(c->h_result);
+    if (c->d_pseudo) (void)hipFree(c->d_pseudo);
+    if (c->d_flows) (void)hipFree(c->d_flows);
+    delete c;
+    return PIPCK_OK;
+}
+
+int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t init, uint32_t* out) {
+    if (!c || !out || (nseg && !segs)) {
+        set_error("pipck_host_sum: null argument");
+        return PIPCK_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    // stage: [SegRef table][segment bytes, each 16-byte aligned]
+    const size_t table = ((size_t)nseg * sizeof(SegRef) + 15) & ~(size_t)15;
+    size_t need = table;
+    for (uint32_t i = 0; i < nseg; i++) {
+        if (segs[i].len && !segs[i].ptr) {
+            set_error("pipck_host_sum: null segment with nonzero length");
+            return PIPCK_EINVAL;
+        }
+        need += ((size_t)segs[i].len + 15) & ~(size_t)15;
+    }
+    int rc = grow_stage(c, need ? need : 16);
+    if (rc) return rc;
+    SegRef* refs = reinterpret_cast<SegRef*>(c->h_stage);
+    size_t off = table;
+    for (uint32_t i = 0; i < nseg; i++) {
+        refs[i] = SegRef{off - table, segs[i].len, 0};
+        if (segs[i].len) std::memcpy(c->h_stage + off, segs[i].ptr, segs[i].len);
+        off += ((size_t)segs[i].len + 15) & ~(size_t)15;
+    }
+    hipStream_t s = c->stream[0];
+    if (need) PIPCK_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, need, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->d_stage + table,
+                       reinterpret_cast<const SegRef*>(c->d_stage), nseg, init, c->d_result);
+    PIPCK_LAUNCHED("k_exact_chain");
+    PIPCK_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PIPCK_HIP(hipStreamSynchronize(s));
+    *out = *c->h_result;
+    return PIPCK_OK;
+}
+
+void* pipck_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void pipck_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride, uint32_t len, uint64_t n,
+                              int family, const void* h_flows, uint32_t n_flows, uint64_t flow_origin,
+                              uint16_t* h_out) {
+    if (!c || (n && (!h_arena || !h_out)) || (family != 0 && family != 4 && family != 6) ||
+        (family && (!h_flows || !n_flows))) {
+        set_error("pipck_host_checksum_fixed: bad argument");
+        return PIPCK_EINVAL;
+    }
+    if (!n) return PIPCK_OK;
+    if (stride < len) {
+        set_error("pipck_host_checksum_fixed: stride < len");
+        return PIPCK_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const uint32_t* d_pseudo = nullptr;
+    if (family) {
+        const size_t fbytes = (size_t)n_flows * (family == 4 ? sizeof(pipck_flow4) : sizeof(pipck_flow6));
+        if (n_flows > c->flows_cap) {
+            if (c->d_flows) PIPCK_HIP(hipFree(c->d_flows));
+            if (c->d_pseudo) PIPCK_HIP(hipFree(c->d_pseudo));
+            c->d_flows = nullptr;
+            c->d_pseudo = nullptr;
+            c->flows_cap = 0;
+            PIPCK_HIP(hipMalloc(&c->d_flows, (size_t)n_flows * sizeof(pipck_flow6)));
+            PIPCK_HIP(hipMalloc((void**)&c->d_pseudo, (size_t)n_flows * sizeof(uint32_t)));
+            c->flows_cap = n_flows;
+        }
+        PIPCK_HIP(hipMemcpyAsync(c->d_flows, h_flows, fbytes, hipMemcpyHostToDevice, c->stream[0]));
+        int rc = family == 4 ? pipck_flows4_prepare((const pipck_flow4*)c->d_flows, n_flows, c->d_pseudo, c->stream[0])
+                             : pipck_flows6_prepare((const pipck_flow6*)c->d_flows, n_flows, c->d_pseudo, c->stream[0]);
+        if (rc) return rc;
+        PIPCK_HIP(hipEventRecord(c->done[0], c->stream[0]));
+        PIPCK_HIP(hipStreamWaitEvent(c->stream[1], c->done[0], 0));
+        d_pseudo = c->d_pseudo;
+    }
+    // ~64 MiB chunks, double-buffered: chunk k uses stream k%2 (H2D -> kernel -> D2H)
+    const uint64_t per_chunk = std::max<uint64_t>(1, (64ull << 20) / stride);
+    const size_t chunk_bytes = (size_t)(per_chunk * stride);
+    if (chunk_bytes > c->chunk_cap) {
+        for (int i = 0; i < 2; i++) {
+            if (c->d_chunk[i]) PIPCK_HIP(hipFree(c->d_chunk[i]));
+            if (c->d_out[i]) PIPCK_HIP(hipFree(c->d_out[i]));
+            c->d_chunk[i] = nullptr;
+            c->d_out[i] = nullptr;
+        }
+        c->chunk_cap = 0;
+        for (int i = 0; i < 2; i++) {
+            PIPCK_HIP(hipMalloc((void**)&c->d_chunk[i], chunk_bytes));
+            PIPCK_HIP(hipMalloc((void**)&c->d_out[i], per_chunk * sizeof(uint16_t)));
+        }
+        c->chunk_cap = chunk_bytes;
+    }
+    for (uint64_t first = 0, k = 0; first < n; first += per_chunk, k++) {
+        const uint64_t m = std::min<uint64_t>(per_chunk, n - first);
+        const int b = (int)(k & 1);
+        hipStream_t s = c->stream[b];
+        const size_t bytes = (size_t)((m - 1) * stride + len);
+        PIPCK_HIP(hipMemcpyAsync(c->d_chunk[b], (const uint8_t*)h_arena + first * stride, bytes,
+                                 hipMemcpyHostToDevice, s));
+        int rc = pipck_checksum_fixed(c->d_chunk[b], stride, len, m, d_pseudo, n_flows, nullptr, flow_origin + first,
+                                      c->d_out[b], s);
+        if (rc) return rc;
+        PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    }
+    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
+    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
+    return PIPCK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,402 @@
+// pipck_kernels.hip -- batch checksum kernels for MI355X (gfx950) + their C ABI.
+//
+// Hot path: plumk97/pip pip/pip_checksum.cpp:13-148 (pip_standard_checksum and
+// its five wrappers) over batches of packets resident in HBM.  Integer
+// reduction, HBM-read bound: no MFMA, no LDS tiling of the payload.  See
+// pipck_device.hpp for why summing little-endian dwords in any order is exact.
+//
+// Kernels
+//   k_fixed<G,NL>   fixed-stride batches (cfg2/3/5 shapes): a group of G lanes
+//                   per packet, NL 16-byte loads per lane in flight per pass,
+//                   64/G packets per wave, group reduce by cross-lane shuffles.
+//   k_ragged<FIN,U> ragged batches and chain segments (cfg4 shape): each wave
+//                   owns a tile of 64 segments and streams the tile's 16-byte
+//                   chunks flat and coalesced (U rows of 64 chunks in flight),
+//                   mapping chunk -> segment by binary search over the tile's
+//                   chunk prefix in LDS, and reducing by segment with a wave
+//                   prefix scan; per-segment partials accumulate in LDS.
+//   k_chain_finish  per-packet fold of chain-segment partials + pseudo-header.
+#include "pipck_common.hpp"
+#include "pipck_device.hpp"
+
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+namespace pipck {
+
+// ---------------------------------------------------------------------------
+// flows -> pseudo-header bases
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t addr_terms(uint32_t s_addr_mem) {
+    uint32_t a = __builtin_bswap32(s_addr_mem);  // ntohl, pip_checksum.cpp:47
+    return (a >> 16) + (a & 0xFFFFu);
+}
+
+__global__ void k_flows4(const pipck_flow4* __restrict__ f, uint32_t n, uint32_t* __restrict__ pseudo) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    pipck_flow4 x = f[i];
+    pseudo[i] = addr_terms(x.src) + addr_terms(x.dst) + x.proto;
+}
+
+__global__ void k_flows6(const pipck_flow6* __restrict__ f, uint32_t n, uint32_t* __restrict__ pseudo) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&f[i]);  // src[4] dst[4] proto
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) s += addr_terms(w[k]);
+    pseudo[i] = s + f[i].proto;
+}
+
+// ---------------------------------------------------------------------------
+// fixed-stride kernel
+// ---------------------------------------------------------------------------
+template <int G, int NL, bool VERIFY>
+__global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
+                                               uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    constexpr int GPB = 256 / G;  // packets per block per iteration
+    const int sub = threadIdx.x % G;
+    uint64_t pkt = (uint64_t)blockIdx.x * GPB + threadIdx.x / G;
+    const uint64_t step = (uint64_t)gridDim.x * GPB;
+    const uint32_t lterm = len_term(len);
+    const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
+    uint32_t flow = 0, flow_step = 0;
+    if (implicit_flow) {  // one 64-bit modulo per thread, then incremental
+        flow = (uint32_t)((flow_origin + pkt) % n_flows);
+        flow_step = (uint32_t)(step % n_flows);
+    }
+    for (; pkt < n; pkt += step) {
+        const uintptr_t addr = (uintptr_t)arena + pkt * stride;
+        const int head = (int)(addr & 15);
+        const u32x4* base = reinterpret_cast<const u32x4*>(addr - head);
+        const int end = head + (int)len;  // one past the last byte, relative to base
+        const int nch = len ? (end + 15) >> 4 : 0;
+        uint64_t acc = 0;
+        for (int cb = 0; cb < nch; cb += G * NL) {  // one pass for packets <= G*NL*16 bytes
+            u32x4 v[NL];
+#pragma unroll
+            for (int k = 0; k < NL; k++) {
+                const int c = cb + k * G + sub;
+                v[k] = c < nch ? load_stream(base + c) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < NL; k++) {
+                const int c = cb + k * G + sub;
+                const int lo = c == 0 ? head : 0;
+                const int hi = end - 16 * c;
+                u32x4 x = v[k];
+                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+                acc += sum4(x);
+            }
+        }
+        uint32_t s = fold64(acc);
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, G);
+        if (sub == 0) {
+            const uint32_t F = be_fold(s, addr);
+            uint32_t P = 0;
+            if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : flow] + lterm;
+            if (VERIFY)
+                ok[pkt] = fold16(P + F) == 0xFFFFu;
+            else
+                out[pkt] = finish(P, F);
+        }
+        if (implicit_flow) {
+            flow += flow_step;
+            if (flow >= n_flows) flow -= n_flows;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ragged / chain-segment kernel
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+template <bool FINAL, int U>
+__global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ arena, const pipck_desc* __restrict__ desc,
+                                                uint64_t n, const uint32_t* __restrict__ pseudo,
+                                                uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
+                                                uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_pre[4][64];   // exclusive chunk prefix of the tile's segments
+    __shared__ uint32_t s_acc[4][64];   // LE residue partial per segment
+    __shared__ uint32_t s_span[4][64];  // (end << 4) | head, relative to the aligned base
+    __shared__ uint64_t s_base[4][64];  // 16-byte-aligned base address of each segment
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t tstep = (uint64_t)gridDim.x * 4;
+    for (uint64_t tile = (uint64_t)blockIdx.x * 4 + w; tile * 64 < n; tile += tstep) {
+        const uint64_t seg = tile * 64 + lane;
+        const bool valid = seg < n;
+        pipck_desc d = valid ? desc[seg] : pipck_desc{0, 0, 0};
+        const bool bad = d.len > PIPCK_MAX_SEG_LEN;
+        const uint32_t len = bad ? 0u : d.len;
+        const uintptr_t addr = (uintptr_t)arena + d.offset;
+        const uint32_t head = (uint32_t)(addr & 15);
+        const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
+        const uint32_t incl = wave_incl_scan(nch, lane);
+        const uint32_t total = __shfl(incl, 63, 64);
+        s_pre[w][lane] = incl - nch;
+        s_span[w][lane] = ((head + len) << 4) | head;
+        s_base[w][lane] = addr - head;
+        s_acc[w][lane] = 0;
+        wave_sync();
+        for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
+            u32x4 v[U];
+            uint32_t sx[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t c = c0 + u * 64 + lane;
+                uint32_t s = 0;  // last segment whose first chunk is <= c (skips empty segments)
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (s_pre[w][s + st] <= c) s += st;
+                sx[u] = s;
+                const u32x4* p = reinterpret_cast<const u32x4*>(s_base[w][s]) + (c - s_pre[w][s]);
+                v[u] = c < total ? load_stream(p) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t row = c0 + u * 64;
+                const uint32_t c = row + lane;
+                const bool active = c < total;
+                const uint32_t s = sx[u];
+                const uint32_t pre = s_pre[w][s];
+                const uint32_t span = s_span[w][s];
+                const int rel = (int)(c - pre);
+                const int lo = rel == 0 ? (int)(span & 15) : 0;
+                const int hi = (int)(span >> 4) - 16 * rel;
+                u32x4 x = v[u];
+                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+                const uint32_t val = active ? fold64(sum4(x)) : 0u;
+                const uint32_t inc = wave_incl_scan(val, lane);
+                const uint32_t s_next = __shfl_down(s, 1, 64);
+                const bool tail = active && (lane == 63 || c + 1 >= total || s_next != s);
+                const int head_lane = (int)pre - (int)row;  // lane holding the segment's first chunk in this row
+                const uint32_t before = __shfl(inc, max(head_lane, 1) - 1, 64);
+                if (tail) atomicAdd(&s_acc[w][s], inc - (head_lane > 0 ? before : 0u));
+            }
+        }
+        wave_sync();
+        if (valid) {
+            const uint32_t F = bad ? 0u : be_fold(s_acc[w][lane], addr);
+            if (FINAL) {
+                const uint32_t P = pseudo ? pseudo[d.flow] + len_term(len) : 0u;
+                out[seg] = bad ? (uint16_t)0 : finish(P, F);
+            } else {
+                fseg[seg] = F;
+            }
+            if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
+        }
+        wave_sync();
+    }
+}
+
+__global__ void k_chain_finish(const pipck_desc* __restrict__ segs, const uint64_t* __restrict__ seg_begin,
+                               const uint32_t* __restrict__ pkt_flow, uint64_t n_pkts,
+                               const uint32_t* __restrict__ pseudo, const uint32_t* __restrict__ fseg,
+                               uint16_t* __restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pkts) return;
+    uint32_t total_len = 0, F = 0;  // pip_buf::total_len is a u32 (pip/pip_buf.h:17)
+    for (uint64_t s = seg_begin[p], e = seg_begin[p + 1]; s < e; s++) {
+        total_len += segs[s].len;
+        F += fseg[s];
+    }
+    const uint32_t P = pseudo ? pseudo[pkt_flow ? pkt_flow[p] : 0u] + len_term(total_len) : 0u;
+    out[p] = finish(P, F);
+}
+
+// ---------------------------------------------------------------------------
+// launch-shape selection
+// ---------------------------------------------------------------------------
+static std::atomic<uint32_t> g_tune_lanes{0}, g_tune_blocks{0};
+
+typedef void (*fixed_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
+                         uint64_t, uint16_t*, uint8_t*);
+struct Variant {
+    int g, nl;
+    fixed_fn sum, verify;
+};
+#define PIPCK_V(G, NL) {G, NL, k_fixed<G, NL, false>, k_fixed<G, NL, true>}
+static const Variant kVariants[] = {
+    PIPCK_V(1, 1),  PIPCK_V(1, 2),  PIPCK_V(2, 1),  PIPCK_V(2, 2),  PIPCK_V(4, 1),  PIPCK_V(4, 2),
+    PIPCK_V(4, 4),  PIPCK_V(8, 2),  PIPCK_V(8, 4),  PIPCK_V(16, 2), PIPCK_V(16, 4), PIPCK_V(16, 6),
+    PIPCK_V(32, 3), PIPCK_V(32, 4), PIPCK_V(64, 2), PIPCK_V(64, 4), PIPCK_V(64, 6), PIPCK_V(64, 9),
+};
+#undef PIPCK_V
+
+// Pick the shape that wastes the fewest 16-byte lane slots, then the one with
+// the most loads in flight per lane, then the widest group.
+static const Variant& pick_variant(uint32_t nch) {
+    const uint32_t forced = g_tune_lanes.load();
+    const Variant* best = nullptr;
+    double best_u = -1.0;
+    for (const Variant& v : kVariants) {
+        if (forced && (uint32_t)v.g != forced) continue;
+        const uint32_t per = (uint32_t)(v.g * v.nl);
+        const uint32_t passes = nch ? (nch + per - 1) / per : 1;
+        const double u = nch ? (double)nch / (double)(per * passes) : 1.0;
+        const bool better = !best || u > best_u + 0.01 ||
+                            (u > best_u - 0.01 && (v.nl > best->nl || (v.nl == best->nl && v.g > best->g)));
+        if (better) {
+            best = &v;
+            best_u = u;
+        }
+    }
+    return best ? *best : kVariants[sizeof(kVariants) / sizeof(kVariants[0]) - 1];
+}
+
+static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n) {
+    uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
+    uint64_t cap = g_tune_blocks.load();
+    if (!cap) cap = (uint64_t)device_cus() * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU
+    if (need > cap) need = cap;
+    return (uint32_t)(need ? need : 1);
+}
+
+static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
+                        const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
+                        uint16_t* d_out, uint8_t* d_ok, void* stream) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || (verify ? !d_ok : !d_out)) {
+        set_error("pipck_checksum_fixed: null arena/output");
+        return PIPCK_EINVAL;
+    }
+    if (len > PIPCK_MAX_SEG_LEN) {
+        set_error("pipck_checksum_fixed: len > 65535 is outside the batch domain");
+        return PIPCK_ERANGE;
+    }
+    if (d_pseudo && !d_flow_of && n_flows == 0) {
+        set_error("pipck_checksum_fixed: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
+    if (stride < len && n > 1) {
+        set_error("pipck_checksum_fixed: stride < len");
+        return PIPCK_EINVAL;
+    }
+    const bool aligned = ((uintptr_t)d_arena % 16 == 0) && (stride % 16 == 0);
+    const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;
+    const Variant& v = pick_variant(nch);
+    const uint32_t grid = grid_for(256 / v.g, n);
+    fixed_fn fn = verify ? v.verify : v.sum;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena, stride, len, n,
+                       d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
+    PIPCK_LAUNCHED("k_fixed");
+    return PIPCK_OK;
+}
+
+constexpr int kRaggedU = 4;
+
+static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_desc, uint64_t n,
+                         const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint32_t* d_err,
+                         hipStream_t s) {
+    const uint64_t tiles = (n + 63) / 64;
+    const uint32_t grid = grid_for(4, tiles);
+    if (final_)
+        hipLaunchKernelGGL((k_ragged<true, kRaggedU>), dim3(grid), dim3(256), 0, s, (const uint8_t*)d_arena, d_desc, n,
+                           d_pseudo, d_out, d_fseg, d_err);
+    else
+        hipLaunchKernelGGL((k_ragged<false, kRaggedU>), dim3(grid), dim3(256), 0, s, (const uint8_t*)d_arena, d_desc,
+                           n, d_pseudo, d_out, d_fseg, d_err);
+    PIPCK_LAUNCHED("k_ragged");
+    return PIPCK_OK;
+}
+
+}  // namespace pipck
+
+using namespace pipck;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+uint32_t pipck_version(void) { return (1u << 16) | 0u; }
+
+void pipck_tune(uint32_t lanes_per_packet, uint32_t blocks) {
+    g_tune_lanes.store(lanes_per_packet);
+    g_tune_blocks.store(blocks);
+}
+
+int pipck_flows4_prepare(const pipck_flow4* d_flows, uint32_t n, uint32_t* d_pseudo, void* stream) {
+    if (!n) return PIPCK_OK;
+    if (!d_flows || !d_pseudo) {
+        set_error("pipck_flows4_prepare: null pointer");
+        return PIPCK_EINVAL;
+    }
+    hipLaunchKernelGGL(k_flows4, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), d_flows, n, d_pseudo);
+    PIPCK_LAUNCHED("k_flows4");
+    return PIPCK_OK;
+}
+
+int pipck_flows6_prepare(const pipck_flow6* d_flows, uint32_t n, uint32_t* d_pseudo, void* stream) {
+    if (!n) return PIPCK_OK;
+    if (!d_flows || !d_pseudo) {
+        set_error("pipck_flows6_prepare: null pointer");
+        return PIPCK_EINVAL;
+    }
+    hipLaunchKernelGGL(k_flows6, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream), d_flows, n, d_pseudo);
+    PIPCK_LAUNCHED("k_flows6");
+    return PIPCK_OK;
+}
+
+int pipck_checksum_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
+                         uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
+                         void* stream) {
+    return launch_fixed(false, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, nullptr,
+                        stream);
+}
+
+int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
+                       uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok,
+                       void* stream) {
+    return launch_fixed(true, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr, d_ok,
+                        stream);
+}
+
+int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
+                          uint16_t* d_out, uint32_t* d_err, void* stream) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_desc || !d_out) {
+        set_error("pipck_checksum_ragged: null pointer");
+        return PIPCK_EINVAL;
+    }
+    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, d_out, nullptr, d_err, as_stream(stream));
+}
+
+int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
+                          const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo,
+                          uint32_t* d_scratch, uint16_t* d_out, uint32_t* d_err, void* stream) {
+    if (n_packets == 0) return PIPCK_OK;
+    if (!d_seg_begin || !d_out || (n_segs && (!d_arena || !d_segs || !d_scratch))) {
+        set_error("pipck_checksum_chains: null pointer");
+        return PIPCK_EINVAL;
+    }
+    hipStream_t s = as_stream(stream);
+    if (n_segs) {
+        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, d_err, s);
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_segs, d_seg_begin,
+                       d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out);
+    PIPCK_LAUNCHED("k_chain_finish");
+    return PIPCK_OK;
+}
+
+}  // extern "C"

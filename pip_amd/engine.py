@@ -1,0 +1,164 @@
+"""Device-resident batch engine: thin Python over the C ABI of libpipck.so.
+
+PyTorch is plumbing here -- it owns device memory, the current HIP stream and
+the multi-process runtime; every byte of checksum work is done by the HIP
+kernels in ``pip_amd/csrc``.  Results are host-order u16 (what pip's
+functions return before the caller's ``htons``), stored in int16 tensors.
+
+Reference interface mirrored: ``pip/pip_checksum.h:17-34`` -- the batch calls
+compute, for every packet of a batch, exactly what ``pip_ip_checksum``,
+``pip_inet_checksum``/``pip_inet6_checksum`` or their ``_buf`` chain variants
+return for that packet.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from . import _lib
+from ._lib import Desc, Flow4, Flow6, call, load  # noqa: F401  (re-exported)
+
+DESC_BYTES = C.sizeof(Desc)  # 16: u64 offset, u32 len, u32 flow
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _ptr(t) -> C.c_void_p | None:
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def current_stream(device=None) -> C.c_void_p:
+    torch = _torch()
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu() -> None:
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise RuntimeError("pip_amd engine needs a HIP device (gfx950); none is visible")
+    load()
+
+
+# ---------------------------------------------------------------- flows
+def gen_flows(family: int, n_flows: int, seed: int, proto: int, device=None):
+    """Synthetic flow table on the device + its pseudo-header bases."""
+    torch = _torch()
+    size = C.sizeof(Flow4 if family == 4 else Flow6)
+    flows = torch.empty(n_flows * size, dtype=torch.uint8, device=device or "cuda")
+    fn = "pipck_gen_flows4" if family == 4 else "pipck_gen_flows6"
+    call(fn, _ptr(flows), n_flows, seed, proto, current_stream(flows.device))
+    return flows, prepare_flows(family, flows, n_flows)
+
+
+def prepare_flows(family: int, flows, n_flows: int):
+    """flows: device uint8 tensor of n_flows pipck_flow4/pipck_flow6 records."""
+    torch = _torch()
+    pseudo = torch.empty(n_flows, dtype=torch.int32, device=flows.device)
+    fn = "pipck_flows4_prepare" if family == 4 else "pipck_flows6_prepare"
+    call(fn, _ptr(flows), n_flows, _ptr(pseudo), current_stream(flows.device))
+    return pseudo
+
+
+def flows_to_device(family: int, flows_bytes: bytes, device=None):
+    torch = _torch()
+    t = torch.frombuffer(bytearray(flows_bytes), dtype=torch.uint8).to(device or "cuda")
+    return t
+
+
+# ---------------------------------------------------------------- batches
+def checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
+                   flow_origin: int = 0, out=None):
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    _check_span(arena, stride, length, n)
+    call("pipck_checksum_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
+         flow_origin, _ptr(out), current_stream(arena.device))
+    return out
+
+
+def verify_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
+                 flow_origin: int = 0, ok=None):
+    torch = _torch()
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check_span(arena, stride, length, n)
+    call("pipck_verify_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
+         flow_origin, _ptr(ok), current_stream(arena.device))
+    return ok
+
+
+def checksum_ragged(arena, desc, pseudo=None, out=None, err=None):
+    """desc: device int64 tensor (n, 2) laid out as pipck_desc."""
+    torch = _torch()
+    n = desc.shape[0]
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    call("pipck_checksum_ragged", _ptr(arena), _ptr(desc), n, _ptr(pseudo), _ptr(out), _ptr(err),
+         current_stream(arena.device))
+    return out
+
+
+def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
+    """segs: (n_segs, 2) int64 descriptors; seg_begin: (n_packets+1,) int64 CSR offsets."""
+    torch = _torch()
+    n_pk = seg_begin.shape[0] - 1
+    scratch = torch.empty(max(segs.shape[0], 1), dtype=torch.int32, device=arena.device)
+    if out is None:
+        out = torch.empty(n_pk, dtype=torch.int16, device=arena.device)
+    call("pipck_checksum_chains", _ptr(arena), _ptr(segs), segs.shape[0], _ptr(seg_begin), _ptr(pkt_flow), n_pk,
+         _ptr(pseudo), _ptr(scratch), _ptr(out), _ptr(err), current_stream(arena.device))
+    return out
+
+
+def _check_span(arena, stride, length, n):
+    """Host-side guard: the kernels must never read past the arena."""
+    if n and (n - 1) * stride + length > arena.numel() * arena.element_size():
+        raise ValueError(f"arena of {arena.numel() * arena.element_size()} B is too small for "
+                         f"{n} packets x stride {stride} (len {length})")
+
+
+def make_desc(offsets, lengths, flows, device=None):
+    """Pack host arrays into a (n, 2) int64 device tensor of pipck_desc."""
+    import numpy as np
+
+    torch = _torch()
+    n = len(offsets)
+    raw = np.zeros(n, dtype=[("offset", "<u8"), ("len", "<u4"), ("flow", "<u4")])
+    raw["offset"], raw["len"], raw["flow"] = offsets, lengths, flows
+    return torch.from_numpy(raw.view(np.int64).reshape(n, 2).copy()).to(device or "cuda")
+
+
+# ---------------------------------------------------------------- generators
+def cfg_seed(cfg: int) -> int:
+    return load().pipck_cfg_seed(cfg)
+
+
+def gen_fixed(arena, stride: int, length: int, n: int, first: int, seed: int, hdr: int) -> None:
+    _check_span(arena, stride, length, n)
+    if n and (n * stride) > arena.numel() * arena.element_size():
+        raise ValueError("arena too small for generated stride slots")
+    call("pipck_gen_fixed", _ptr(arena), stride, length, n, first, seed, hdr, current_stream(arena.device))
+
+
+def gen_ragged(n: int, first: int, seed: int, hdr: int, n_flows: int, device=None, lengths=None):
+    """Zipf-length batch (cfg4 shape). Returns (arena, desc, lengths)."""
+    torch = _torch()
+    dev = device or "cuda"
+    if lengths is None:
+        lengths = torch.empty(n, dtype=torch.int32, device=dev)
+        call("pipck_gen_zipf_lengths", _ptr(lengths), n, first, seed, current_stream(lengths.device))
+    desc = torch.empty((n, 2), dtype=torch.int64, device=lengths.device)
+    nbytes = C.c_uint64(0)
+    call("pipck_gen_ragged_layout", _ptr(lengths), n, first, n_flows, _ptr(desc), C.byref(nbytes),
+         current_stream(lengths.device))
+    arena = torch.empty(max(int(nbytes.value), 16), dtype=torch.uint8, device=lengths.device)
+    call("pipck_gen_ragged_fill", _ptr(arena), _ptr(desc), n, first, seed, hdr, current_stream(arena.device))
+    return arena, desc, lengths
+
+
+def tune(lanes_per_packet: int = 0, blocks: int = 0) -> None:
+    load().pipck_tune(lanes_per_packet, blocks)

@@ -1,0 +1,107 @@
+"""Sharding of packet batches across GPUs.
+
+Every packet is independent, so a batch is split into contiguous global
+packet-id ranges, one per rank (one process per GPU).  There is no exchange
+step and therefore no collective on the data path: each rank generates its
+own shard on its own device from global packet ids and checksums it in
+place.  The only cross-rank traffic is control: a barrier around the timed
+region and a MAX of the per-rank elapsed times, over gloo (CPU), so RCCL is
+never initialised.
+"""
+from __future__ import annotations
+
+import os
+from bisect import bisect_left
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class DistEnv:
+    rank: int
+    world: int
+    local_rank: int
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+def dist_env() -> DistEnv:
+    """RANK / WORLD_SIZE / LOCAL_RANK as set by torch.distributed.run."""
+    return DistEnv(int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+                   int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous, balanced packet-id range [first, first+count) of one rank."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    first = n_total * rank // world
+    return first, n_total * (rank + 1) // world - first
+
+
+def shard_by_bytes(prefix_bytes: list[int] | tuple[int, ...], world: int, rank: int) -> tuple[int, int]:
+    """Ragged batches: split at packet boundaries so every rank gets ~equal bytes.
+
+    ``prefix_bytes[i]`` is the byte offset where packet i starts; the last
+    element is the total (len == n_packets + 1)."""
+    n = len(prefix_bytes) - 1
+    total = prefix_bytes[-1]
+
+    def cut(r: int) -> int:
+        if r <= 0:
+            return 0
+        if r >= world:
+            return n
+        return min(n, bisect_left(prefix_bytes, total * r // world))
+
+    a, b = cut(rank), cut(rank + 1)
+    return a, b - a
+
+
+def init_control_plane(env: DistEnv) -> None:
+    """gloo process group for the barrier and the MAX of elapsed times."""
+    if not env.distributed:
+        return
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=env.rank, world_size=env.world)
+
+
+def barrier(env: DistEnv) -> None:
+    if env.distributed:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(env: DistEnv, value: float) -> float:
+    if not env.distributed:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(env: DistEnv, value: float) -> float:
+    if not env.distributed:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def shutdown(env: DistEnv) -> None:
+    if env.distributed:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()

@@ -1,0 +1,108 @@
+"""CPU: the drop-in boundary -- the C-ABI library and the C++ shim load and
+export exactly what include/*.h declares; without a GPU they fail loudly."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from pip_amd import _lib
+
+ROOT = Path(__file__).resolve().parents[1]
+
+PIP_MANGLED = [  # SURVEY.md 8b, measured from the reference object
+    "_Z21pip_standard_checksumPKvjj",
+    "_Z15pip_ip_checksumPKvj",
+    "_Z17pip_inet_checksumPKvh7in_addrS1_t",
+    "_Z18pip_inet6_checksumPKvh8in6_addrS1_t",
+    "_Z21pip_inet_checksum_bufSt10shared_ptrI7pip_bufEh7in_addrS2_",
+    "_Z22pip_inet6_checksum_bufSt10shared_ptrI7pip_bufEh8in6_addrS2_",
+    "_Z15pip_fold_uint32j",
+]
+
+
+def header_functions(path: Path) -> list[str]:
+    text = re.sub(r"/\*.*?\*/", "", path.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(pipck_\w+)\s*\(", text, flags=re.M)))
+
+
+def dynsyms(path: Path) -> set[str]:
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_libpipck_exports_every_declared_function():
+    declared = header_functions(ROOT / "include" / "pipck.h")
+    assert len(declared) >= 20
+    syms = dynsyms(_lib.LIBPIPCK)
+    missing = [f for f in declared if f not in syms]
+    assert not missing, missing
+    # and the ctypes table covers the header exactly
+    assert sorted(_lib.SIGNATURES) == declared
+
+
+def test_libpipck_loads_and_reports_version():
+    lib = _lib.load()
+    assert lib.pipck_version() >> 16 == 1
+    assert lib.pipck_cfg_seed(5) == 0x9E3779B97F4A7C15 ^ 5
+
+
+def test_kernels_are_built_for_gfx950_only():
+    blob = _lib.LIBPIPCK.read_bytes()
+    assert b"gfx950" in blob
+    for other in (b"gfx942", b"gfx90a", b"gfx1100"):
+        assert b"amdgcn-amd-amdhsa--" + other not in blob
+
+
+def test_shim_exports_pip_mangled_names():
+    syms = dynsyms(_lib.LIBSHIM)
+    assert set(PIP_MANGLED) <= syms
+    needed = subprocess.run(["readelf", "-d", str(_lib.LIBSHIM)], check=True, capture_output=True, text=True).stdout
+    assert "libpipck.so" in needed
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    lib = _lib.load()
+    ctx = C.c_void_p()
+    rc = lib.pipck_ctx_create(-1, C.byref(ctx))
+    assert rc == _lib.PIPCK_ENODEV
+    assert b"no HIP device" in lib.pipck_last_error()
+    from pip_amd import engine
+
+    with pytest.raises(RuntimeError):
+        engine.require_gpu()
+    # the per-packet API has no host path either
+    from pip_amd import checksum
+
+    with pytest.raises(_lib.PipckError):
+        checksum.pip_ip_checksum(bytes(20))
+
+
+def test_shim_aborts_without_gpu():
+    """pip's API has no error channel: the drop-in prints and aborts rather than
+    computing anywhere else (pip_checksum_shim.cpp)."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    prog = ROOT / "oracle" / "_ref" / "stack_replay_amd"
+    if not prog.exists():
+        pytest.skip("replay driver not built (needs /root/reference)")
+    r = subprocess.run([str(prog)], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "libpip_checksum_amd" in r.stderr
+
+
+def test_batch_abi_rejects_out_of_domain_arguments():
+    lib = _lib.load()
+    # len > 65535 is outside the batch domain -> ERANGE before anything launches
+    rc = lib.pipck_checksum_fixed(C.c_void_p(16), 70000, 70000, 1, None, 1, None, 0, C.c_void_p(16), None)
+    assert rc == _lib.PIPCK_ERANGE
+    rc = lib.pipck_checksum_fixed(None, 16, 16, 1, None, 1, None, 0, C.c_void_p(16), None)
+    assert rc == _lib.PIPCK_EINVAL
+    assert lib.pipck_checksum_fixed(None, 16, 16, 0, None, 1, None, 0, None, None) == _lib.PIPCK_OK

@@ -1,0 +1,37 @@
+"""GPU: link-substitution boundary test.
+
+oracle/_ref/stack_replay_amd is pip's REAL TCP/UDP/IP stack (compiled from
+/root/reference without pip_checksum.cpp) linked against the product's
+libpip_checksum_amd.so.  It replays a scripted exchange -- IPv4 and IPv6 TCP
+handshakes (SYN-ACK with its 8-byte option segment), multi-segment writes,
+odd-length data, UDP over v4/v6 with odd and jumbo payloads, all-zero and
+all-0xFF datagrams -- and prints every IP packet pip emits.  The bytes must
+equal what pip emits with its own pip_checksum.cpp (tests/golden/stack_replay.txt,
+recorded from oracle/_ref/stack_replay_ref).
+"""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+REPLAY_AMD = ROOT / "oracle" / "_ref" / "stack_replay_amd"
+GOLDEN = ROOT / "tests" / "golden" / "stack_replay.txt"
+
+
+def test_golden_replay_is_self_consistent():
+    lines = GOLDEN.read_text().strip().splitlines()
+    assert lines[-1] == f"PACKETS {len(lines) - 1} VERIFY_BAD 0"
+    assert len(lines) - 1 >= 25
+
+
+@pytest.mark.gpu
+def test_pip_stack_on_amd_checksum_is_byte_identical():
+    assert REPLAY_AMD.exists(), "build with `make -C oracle ref ref-amd` where /root/reference exists"
+    r = subprocess.run([str(REPLAY_AMD)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = GOLDEN.read_text().strip().splitlines()
+    got = r.stdout.strip().splitlines()
+    assert got[-1] == want[-1]
+    diff = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
+    assert not diff and len(got) == len(want), diff[:5]

@@ -1,0 +1,426 @@
+"""GPU parity: the HIP kernels vs pip (golden fixtures) and vs the oracle.
+
+Everything here runs through libpipck.so on a real MI355X.  Bit-exact is the
+bar (integer work).  Sizes: the oracle comparisons use batches the CPU
+oracle finishes in seconds; the full BASELINE.json sizes are checked through
+size-independent properties (a sampled oracle comparison + checksum-of-checksum:
+writing each result into its packet's checksum field must make the packet sum
+to 0xFFFF, i.e. recompute to 0x0000 and verify as valid).
+"""
+import ctypes as C
+import hashlib
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from pip_amd import _lib, engine  # noqa: E402
+from pip_amd import checksum as pc  # noqa: E402
+from pip_amd.workloads import ALL, CFG1, CFG2, CFG3, CFG4, CFG5, N_FLOWS  # noqa: E402
+from tests.golden.make_golden import run_case  # noqa: E402
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    engine.require_gpu()
+    yield
+    engine.tune(0, 0)
+    torch.cuda.synchronize()
+
+
+def u16(t) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint16)
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def upload(buf: np.ndarray, misalign: int = 0):
+    """Device copy of host bytes starting `misalign` bytes past a 256-B aligned base."""
+    t = torch.zeros(buf.size + misalign + 64, dtype=torch.uint8, device=DEV)
+    view = t[misalign:misalign + buf.size]
+    view.copy_(torch.from_numpy(buf))
+    return t, view
+
+
+class PcAdapter:
+    """run_case() adapter: pip's per-packet API on the GPU (pip_amd.checksum)."""
+
+    standard_checksum = staticmethod(lambda d, n, s: pc.pip_standard_checksum(d, n, s))
+    ip_checksum = staticmethod(lambda d, n=None: pc.pip_ip_checksum(d, n))
+    fold_uint32 = staticmethod(pc.pip_fold_uint32)
+    inet_checksum = staticmethod(lambda d, p, s, t, n=None: pc.pip_inet_checksum(d, p, s, t, n))
+    inet6_checksum = staticmethod(lambda d, p, s, t, n=None: pc.pip_inet6_checksum(d, p, s, t, n))
+    inet_checksum_chain = staticmethod(pc.pip_inet_checksum_buf)
+    inet6_checksum_chain = staticmethod(pc.pip_inet6_checksum_buf)
+
+
+# ----------------------------------------------------------------------------
+# 1. pip's known answers through the per-packet (exact) device path
+# ----------------------------------------------------------------------------
+def test_every_known_answer_on_gpu(kat):
+    bad = []
+    for c in kat:
+        got = run_case(PcAdapter, c)
+        if got != c["expect"]:
+            bad.append((c["fn"], c.get("data", c.get("segs")), c["expect"], got))
+    assert not bad, bad[:5]
+
+
+def test_per_packet_api_is_thread_safe(kat):
+    cases = [c for c in kat if c["fn"] != "fold"][:60]
+    errors = []
+
+    def worker():
+        try:
+            for c in cases:
+                if run_case(PcAdapter, c) != c["expect"]:
+                    errors.append(c)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=worker) for _ in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+
+
+# ----------------------------------------------------------------------------
+# 2. device generator == fixture bytes; batch kernels == pip's results
+# ----------------------------------------------------------------------------
+def _device_batch(b, w):
+    if w.ragged:
+        arena, desc, lens = engine.gen_ragged(b["n"], b["first"], b["seed"], b["hdr"], N_FLOWS)
+        return arena, desc, lens
+    arena = torch.empty(b["n"] * b["stride"], dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, b["stride"], b["length"], b["n"], b["first"], b["seed"], b["hdr"])
+    return arena, None, None
+
+
+def _pseudo(w, first=0):
+    if not w.family:
+        return None
+    _, pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)
+    return pseudo
+
+
+@pytest.mark.parametrize("name", sorted(ALL))
+def test_generator_reproduces_fixture_bytes(batches, name):
+    b, w = batches[name], ALL[name]
+    arena, desc, lens = _device_batch(b, w)
+    torch.cuda.synchronize()
+    if w.ragged:
+        assert sha(lens.cpu().numpy().astype("<u4")) == b["lengths_sha256"]
+        assert arena.numel() == b["arena_bytes"]
+    assert sha(arena.cpu().numpy()) == b["arena_sha256"]
+
+
+@pytest.mark.parametrize("name", sorted(ALL))
+def test_batch_kernel_reproduces_pips_results(batches, name):
+    b, w = batches[name], ALL[name]
+    arena, desc, _ = _device_batch(b, w)
+    pseudo = _pseudo(w)
+    if w.ragged:
+        out = engine.checksum_ragged(arena, desc, pseudo)
+    else:
+        out = engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None, b["first"])
+    got = u16(out)
+    assert list(got[:16]) == b["head"]
+    assert sha(got.astype("<u2")) == b["results_sha256"]
+
+
+def test_device_flows_match_oracle(oracle):
+    for fam, proto in ((4, 6), (6, 17)):
+        seed = 0x1234 + fam
+        flows, pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)
+        want = oracle.flows_table(fam, seed, N_FLOWS, proto)
+        assert flows.cpu().numpy().tobytes() == want
+        # pseudo base from a host-uploaded table equals the device-generated one
+        t = engine.flows_to_device(fam, want)
+        assert torch.equal(engine.prepare_flows(fam, t, N_FLOWS), pseudo)
+
+
+# ----------------------------------------------------------------------------
+# 3. fixed-stride kernel: every launch shape, lengths, strides, alignments
+# ----------------------------------------------------------------------------
+LENGTHS = [0, 1, 2, 3, 15, 16, 17, 20, 31, 33, 64, 100, 1023, 1024, 1025, 1480, 4095, 8960, 8980, 9216, 9217,
+           20001, 65535]
+
+
+@pytest.mark.parametrize("lanes", [0, 1, 2, 4, 8, 16, 32, 64])
+def test_fixed_every_shape_vs_oracle(oracle, lanes):
+    rng = np.random.default_rng(100 + lanes)
+    engine.tune(lanes, 0)
+    try:
+        for length in LENGTHS:
+            for fam in (0, 4, 6):
+                stride = int(rng.choice([length, (length + 7) // 8 * 8, (length + 15) // 16 * 16 + 16, length + 1]))
+                stride = max(stride, 1)
+                n = int(rng.integers(1, 40)) if length > 9000 else int(rng.integers(60, 300))
+                misalign = int(rng.integers(0, 16))
+                host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+                if rng.random() < 0.3:  # sprinkle all-0xFF / all-zero packets
+                    host[:stride] = 0xFF
+                    host[-stride:] = 0
+                _, arena = upload(host, misalign)
+                seed, proto, origin = int(rng.integers(0, 2**63)), int(rng.integers(0, 256)), int(rng.integers(0, 5000))
+                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+                out = engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin)
+                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+                got = u16(out)
+                assert np.array_equal(got, want), (lanes, length, stride, fam, misalign,
+                                                   np.nonzero(got != want)[0][:5])
+    finally:
+        engine.tune(0, 0)
+
+
+def test_fixed_grid_stride_loop(oracle):
+    """Force a tiny grid so every block loops over many packets."""
+    rng = np.random.default_rng(5)
+    host = rng.integers(0, 256, 5000 * 1488, dtype=np.uint8)
+    _, arena = upload(host)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, 77, 6)
+    want = oracle.batch_fixed(host, 1488, 1480, 5000, 4, 6, 77, N_FLOWS, 123)
+    for blocks in (1, 3, 17):
+        engine.tune(0, blocks)
+        try:
+            got = u16(engine.checksum_fixed(arena, 1488, 1480, 5000, pseudo, N_FLOWS, None, 123))
+        finally:
+            engine.tune(0, 0)
+        assert np.array_equal(got, want), blocks
+
+
+def test_fixed_explicit_flow_indices(oracle):
+    rng = np.random.default_rng(6)
+    n, L = 777, 333
+    host = rng.integers(0, 256, n * L, dtype=np.uint8)
+    _, arena = upload(host)
+    flows, pseudo = engine.gen_flows(6, N_FLOWS, 99, 17)
+    flow_of = rng.integers(0, N_FLOWS, n).astype(np.int32)
+    got = u16(engine.checksum_fixed(arena, L, L, n, pseudo, N_FLOWS, torch.from_numpy(flow_of).to(DEV), 0))
+    for i in range(n):
+        s, d = oracle.flow6(99, int(flow_of[i]))
+        assert got[i] == oracle.inet6_checksum(host[i * L:(i + 1) * L].tobytes(), 17, s, d)
+
+
+# ----------------------------------------------------------------------------
+# 4. ragged kernel and chains
+# ----------------------------------------------------------------------------
+def _ragged_case(rng, n, max_len=9000, gaps=True):
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[rng.random(n) < 0.1] = 0
+    lens[rng.random(n) < 0.05] = 1
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 40)) if gaps else 0
+        offs[i] = pos
+        pos += int(lens[i])
+    perm = rng.permutation(n)  # descriptors need not be in arena order
+    return offs[perm], lens[perm], pos
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4099])
+def test_ragged_vs_oracle(oracle, n):
+    rng = np.random.default_rng(n)
+    for fam, max_len in ((4, 9000), (6, 65535), (0, 300)):
+        offs, lens, size = _ragged_case(rng, n, max_len)
+        host = rng.integers(0, 256, size + 16, dtype=np.uint8)
+        _, arena = upload(host, int(rng.integers(0, 16)))
+        seed, proto, origin = 4242 + n, 6, int(rng.integers(0, 999))
+        pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+        flows = (origin + np.arange(n)) % N_FLOWS
+        desc = engine.make_desc(offs, lens, flows)
+        got = u16(engine.checksum_ragged(arena, desc, pseudo))
+        want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
+        assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
+
+
+def test_ragged_out_of_domain_flags_error(oracle):
+    rng = np.random.default_rng(9)
+    host = rng.integers(0, 256, 200_000, dtype=np.uint8)
+    _, arena = upload(host)
+    offs = np.array([0, 10, 100_000, 5], dtype=np.uint64)
+    lens = np.array([100, 70_000, 33, 0], dtype=np.uint32)
+    desc = engine.make_desc(offs, lens, np.zeros(4))
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = u16(engine.checksum_ragged(arena, desc, None, err=err))
+    assert int(err.item()) & (1 << _lib.PIPCK_ERANGE)
+    assert got[1] == 0
+    for i in (0, 2, 3):
+        assert got[i] == oracle.ip_checksum(host[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
+
+
+@pytest.mark.parametrize("fam", [4, 6])
+def test_chains_vs_oracle(oracle, fam):
+    """pip_inet{,6}_checksum_buf: odd-length middle segments restart byte pairing."""
+    rng = np.random.default_rng(fam)
+    n_pk = 700
+    seg_lens, seg_begin = [], [0]
+    for _ in range(n_pk):
+        k = int(rng.integers(0, 7))
+        seg_lens += [int(rng.choice([rng.integers(0, 9), rng.integers(0, 3000), 20, 8])) for _ in range(k)]
+        seg_begin.append(len(seg_lens))
+    seg_lens = np.array(seg_lens, dtype=np.uint32)
+    offs = np.zeros(len(seg_lens), dtype=np.uint64)
+    pos = 0
+    for i, L in enumerate(seg_lens):
+        pos += int(rng.integers(0, 17))
+        offs[i] = pos
+        pos += int(L)
+    host = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+    _, arena = upload(host, 3)
+    seed, proto = 31337, 17
+    flows, pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)
+    pkt_flow = rng.integers(0, N_FLOWS, n_pk).astype(np.int32)
+    segs = engine.make_desc(offs, seg_lens, np.zeros(len(seg_lens)))
+    got = u16(engine.checksum_chains(arena, segs, torch.tensor(seg_begin, dtype=torch.int64, device=DEV),
+                                     torch.from_numpy(pkt_flow).to(DEV), pseudo))
+    for p in range(n_pk):
+        chain = [host[int(offs[s]):int(offs[s]) + int(seg_lens[s])].tobytes() for s in range(seg_begin[p], seg_begin[p + 1])]
+        s, d = (oracle.flow4 if fam == 4 else oracle.flow6)(seed, int(pkt_flow[p]))
+        fn = oracle.inet_checksum_chain if fam == 4 else oracle.inet6_checksum_chain
+        assert got[p] == fn(chain, proto, s, d), p
+
+
+# ----------------------------------------------------------------------------
+# 5. RX verification kernel
+# ----------------------------------------------------------------------------
+def test_verify_fixed_accepts_checksummed_and_rejects_corrupted():
+    w = CFG2
+    n = 20000
+    arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, 6)
+    out = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)
+    _insert_fixed(arena, w.stride, n, 16, out)
+    ok = engine.verify_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)
+    assert bool((ok == 1).all())
+    rows = arena.view(n, w.stride)
+    rows[::7, 100] ^= 0x5A
+    ok = engine.verify_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS).cpu().numpy()
+    assert not ok[::7].any() and ok[np.arange(n) % 7 != 0].all()
+
+
+def _insert_fixed(arena, stride, n, field, out):
+    """Store each result big-endian (htons) into its packet's checksum field."""
+    rows = arena.view(n, stride)
+    v = out.to(torch.int32) & 0xFFFF
+    rows[:, field] = (v >> 8).to(torch.uint8)
+    rows[:, field + 1] = (v & 0xFF).to(torch.uint8)
+
+
+# ----------------------------------------------------------------------------
+# 6. host-memory pipeline (H2D -> kernel -> D2H, two streams)
+# ----------------------------------------------------------------------------
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_vs_oracle(oracle, pinned):
+    lib = _lib.load()
+    ctx = C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    try:
+        w = CFG3
+        n = 9000  # > one 64 MiB chunk: exercises double buffering
+        host = oracle.gen_fixed_batch(w.seed, 0, n, w.length, w.hdr, w.stride, 8)
+        flows = oracle.flows_table(6, w.seed, N_FLOWS, w.proto)
+        out = np.zeros(n, dtype=np.uint16)
+        src = host
+        pin = None
+        if pinned:
+            pin = lib.pipck_host_alloc(host.size)
+            C.memmove(pin, host.ctypes.data, host.size)
+            src_ptr = C.c_void_p(pin)
+        else:
+            src_ptr = C.c_void_p(src.ctypes.data)
+        fl = C.create_string_buffer(flows, len(flows))
+        _lib.check("pipck_host_checksum_fixed",
+                   lib.pipck_host_checksum_fixed(ctx, src_ptr, w.stride, w.length, n, 6, fl, N_FLOWS, 0,
+                                                 C.c_void_p(out.ctypes.data)))
+        if pin:
+            lib.pipck_host_free(pin)
+        want = oracle.batch_fixed(host, w.stride, w.length, n, 6, w.proto, w.seed, N_FLOWS, 0, 8)
+        assert np.array_equal(out, want)
+    finally:
+        lib.pipck_ctx_destroy(ctx)
+
+
+# ----------------------------------------------------------------------------
+# 7. generator shard invariance
+# ----------------------------------------------------------------------------
+def test_generator_is_shard_invariant():
+    w = CFG5
+    whole = torch.empty(1000 * w.stride, dtype=torch.uint8, device=DEV)
+    part = torch.empty(400 * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(whole, w.stride, w.length, 1000, 5_000_000, w.seed, w.hdr)
+    engine.gen_fixed(part, w.stride, w.length, 400, 5_000_300, w.seed, w.hdr)
+    assert torch.equal(whole[300 * w.stride:700 * w.stride], part)
+
+
+# ----------------------------------------------------------------------------
+# 8. full BASELINE.json sizes: sampled oracle comparison + checksum-of-checksum
+# ----------------------------------------------------------------------------
+FULL = [(CFG1, 1 << 20, 0), (CFG2, 4 << 20, 0), (CFG3, 1 << 20, 0), (CFG5, 8 << 20, 8 << 20)]
+FIELD = {1: 10, 2: 16, 3: 6, 4: 16, 5: 16}  # ip_sum / th_sum / uh_sum offsets
+
+
+@pytest.mark.parametrize("w,n,first", FULL, ids=[w.name for w, _, _ in FULL])
+def test_full_size_fixed(oracle, w, n, first):
+    arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, w.stride, w.length, n, first, w.seed, w.hdr)
+    pseudo = _pseudo(w)
+    out = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, first)
+    got = u16(out)
+    rng = np.random.default_rng(w.cfg)
+    for i in rng.choice(n, 1500, replace=False):
+        pkt = oracle.packet(w.seed, first + int(i), w.length, w.hdr)
+        f = (first + int(i)) % N_FLOWS
+        if w.family == 4:
+            want = oracle.inet_checksum(pkt, w.proto, *oracle.flow4(w.seed, f))
+        elif w.family == 6:
+            want = oracle.inet6_checksum(pkt, w.proto, *oracle.flow6(w.seed, f))
+        else:
+            want = oracle.ip_checksum(pkt)
+        assert got[i] == want, (w.name, int(i))
+    _insert_fixed(arena, w.stride, n, FIELD[w.cfg], out)
+    again = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, first)
+    assert int((again != 0).sum().item()) == 0
+    ok = engine.verify_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, first)
+    assert bool((ok == 1).all())
+    del arena, out, again, ok
+    torch.cuda.empty_cache()
+
+
+def test_full_size_ragged(oracle):
+    w, n = CFG4, 8 << 20
+    arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    out = engine.checksum_ragged(arena, desc, pseudo)
+    got = u16(out)
+    d = desc.cpu().numpy()
+    offs = d[:, 0].astype(np.uint64)
+    L = (d[:, 1] & 0xFFFFFFFF).astype(np.uint32)
+    assert 900 < L.mean() < 1080
+    rng = np.random.default_rng(4)
+    for i in rng.choice(n, 1500, replace=False):
+        assert L[i] == oracle.zipf_len(w.seed, int(i))
+        pkt = oracle.packet(w.seed, int(i), int(L[i]), w.hdr)
+        assert got[i] == oracle.inet_checksum(pkt, w.proto, *oracle.flow4(w.seed, int(i) % N_FLOWS)), int(i)
+    # checksum-of-checksum over the whole ragged batch
+    o = torch.from_numpy(offs.astype(np.int64)).to(DEV) + 16
+    v = out.to(torch.int32) & 0xFFFF
+    arena[o] = (v >> 8).to(torch.uint8)
+    arena[o + 1] = (v & 0xFF).to(torch.uint8)
+    again = engine.checksum_ragged(arena, desc, pseudo)
+    assert int((again != 0).sum().item()) == 0
+    del arena, desc, out, again
+    torch.cuda.empty_cache()

@@ -1,0 +1,97 @@
+"""CPU: the N>1 path.  Shards are contiguous global packet-id ranges; each rank
+checksums its own shard with no data-path collective; the union over ranks is
+byte- and result-identical to a single-rank run.  world_size 2 over gloo."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from pip_amd import shard
+from pip_amd.workloads import CFG2, CFG4, N_FLOWS
+
+
+def test_shard_range_partitions_exactly():
+    for n in (0, 1, 7, 1000, 64 << 20):
+        for world in (1, 2, 3, 4, 8):
+            parts = [shard.shard_range(n, world, r) for r in range(world)]
+            assert parts[0][0] == 0
+            assert sum(c for _, c in parts) == n
+            for (f0, c0), (f1, _) in zip(parts, parts[1:]):
+                assert f0 + c0 == f1
+            assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+
+
+def test_shard_by_bytes_balances_ragged():
+    rng = np.random.default_rng(3)
+    lens = rng.integers(64, 9000, 5000)
+    prefix = [0] + list(np.cumsum(lens))
+    for world in (1, 2, 4, 8):
+        parts = [shard.shard_by_bytes(prefix, world, r) for r in range(world)]
+        assert sum(c for _, c in parts) == len(lens)
+        per = [prefix[f + c] - prefix[f] for f, c in parts]
+        assert max(per) - min(per) <= 2 * 9000
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from oracle.oracle import Oracle
+
+    env = shard.dist_env()
+    shard.init_control_plane(env)
+    orc = Oracle()
+    n_total = 3000
+    w = CFG2
+    first, count = shard.shard_range(n_total, env.world, env.rank)
+    arena = orc.gen_fixed_batch(w.seed, first, count, w.length, w.hdr, w.stride)
+    out = orc.batch_fixed(arena, w.stride, w.length, count, w.family, w.proto, w.seed, N_FLOWS, first)
+    shard.barrier(env)
+    t = shard.max_over_ranks(env, float(rank + 1))
+    total = shard.sum_over_ranks(env, float(count))
+    q.put((rank, first, out.tobytes(), t, total))
+    shard.shutdown(env)
+
+
+def test_gloo_world2_shards_equal_single_run(oracle):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w = CFG2
+    arena = oracle.gen_fixed_batch(w.seed, 0, 3000, w.length, w.hdr, w.stride)
+    single = oracle.batch_fixed(arena, w.stride, w.length, 3000, w.family, w.proto, w.seed, N_FLOWS, 0)
+    joined = np.frombuffer(b"".join(r[2] for r in res), dtype=np.uint16)
+    assert np.array_equal(joined, single)
+    assert all(r[3] == 2.0 for r in res)      # MAX over ranks
+    assert all(r[4] == 3000.0 for r in res)   # units all ranks processed
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ragged_shards_regenerate_identically(oracle, world):
+    """cfg4: a rank regenerates packets from global ids, so its bytes do not
+    depend on the GPU count."""
+    w = CFG4
+    n = 400
+    whole, offs, lens = oracle.gen_ragged_batch(w.seed, 0, n, w.hdr)
+    for r in range(world):
+        first, count = shard.shard_range(n, world, r)
+        part, poffs, plens = oracle.gen_ragged_batch(w.seed, first, count, w.hdr)
+        assert np.array_equal(plens, lens[first:first + count])
+        for i in range(count):
+            a = whole[int(offs[first + i]):int(offs[first + i]) + int(lens[first + i])]
+            b = part[int(poffs[i]):int(poffs[i]) + int(plens[i])]
+            assert np.array_equal(a, b)

@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> GPU tests -> bench -> rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a crash/abort/timeout stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+stop_if_fatal() {  # $1 = rc, $2 = step; pytest rc 1 = test failures (not fatal)
+  case "$1" in
+    0) ;;
+    1) [ "$2" = pytest ] || { echo "step $2 failed rc=$1"; exit "$1"; } ;;
+    *) echo "step $2 fatal rc=$1 -- stopping"; exit "$1" ;;
+  esac
+}
+STEPS="${STEPS:-smoke pytest bench prof}"
+for s in $STEPS; do
+  echo "== $s $(date +%T)"
+  case "$s" in
+    smoke)  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$? ;;
+    pytest) timeout -k 10 1200 python3 -m pytest tests -m gpu -q -x --durations=15 > "$OUT/pytest_gpu.log" 2>&1; rc=$? ;;
+    bench)  timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$? ;;
+    prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+              python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$? ;;
+    *) echo "unknown step $s"; rc=0 ;;
+  esac
+  echo "   rc=$rc"
+  tail -3 "$OUT/$( [ "$s" = pytest ] && echo pytest_gpu.log || ([ "$s" = smoke ] && echo smoke.log || ([ "$s" = bench ] && echo bench.json || echo prof.err)))" 2>/dev/null
+  stop_if_fatal "$rc" "$s"
+done
+echo "== done $(date +%T)"
