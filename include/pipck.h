@@ -116,9 +116,12 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
                        const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                        uint64_t flow_origin, uint8_t* d_ok, void* stream);
 
-/* Launch-shape override for tuning (0 = automatic).  lanes_per_packet in
- * {1,2,4,8,16,32,64}; blocks = grid size cap. */
-void pipck_tune(uint32_t lanes_per_packet, uint32_t blocks);
+/* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
+ * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
+ * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
+ * in flight); blocks caps the grid; flags bit 0 = plain (cached) loads instead
+ * of non-temporal ones. */
+void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */
 #define PIPCK_HDR_NONE 0
@@ -156,7 +159,8 @@ typedef struct pipck_hseg {
 /* pip's exact sequential semantics over host bytes, computed on the device:
  *   sum = init; for each seg: sum = fold(fold((sum + sum16be(seg)) mod 2^32))
  * (pip_standard_checksum, pip_checksum.cpp:13-33, chained as at :110-112).
- * *out receives the final folded u32 in [0, 0xFFFF].  Synchronous. */
+ * *out receives the final folded u32 in [0, 0xFFFF].  nseg == 0 behaves as one
+ * empty segment (a pip_buf chain is never empty).  Synchronous. */
 int pipck_host_sum(pipck_ctx* ctx, const pipck_hseg* segs, uint32_t nseg, uint32_t init, uint32_t* out);
 
 /* Host-resident fixed-stride batch: H2D in chunks, kernel, D2H of results,

@@ -75,6 +75,9 @@ uint16_t ock_inet_checksum_chain(const void* const* segs, const uint32_t* lens, 
     for (uint32_t s = 0; s < nseg; s++) total += lens[s];
     uint32_t sum = addr4_terms(src) + addr4_terms(dst) + proto + (total >> 16) + (total & 0xFFFFu);
     for (uint32_t s = 0; s < nseg; s++) sum = ock_standard_checksum(segs[s], lens[s], sum);
+    /* pip's chain always holds at least one pip_buf, so its loop folds at least once;
+     * zero segments are treated as one empty segment (as oracle/ref_bridge.cpp builds it). */
+    if (nseg == 0) sum = ock_standard_checksum(NULL, 0, sum);
     return (uint16_t)~(uint16_t)sum;
 }
 
@@ -85,6 +88,7 @@ uint16_t ock_inet6_checksum_chain(const void* const* segs, const uint32_t* lens,
     for (uint32_t s = 0; s < nseg; s++) total += lens[s];
     uint32_t sum = addr6_terms(src) + addr6_terms(dst) + proto + (total >> 16) + (total & 0xFFFFu);
     for (uint32_t s = 0; s < nseg; s++) sum = ock_standard_checksum(segs[s], lens[s], sum);
+    if (nseg == 0) sum = ock_standard_checksum(NULL, 0, sum);
     return (uint16_t)~(uint16_t)sum;
 }
 

@@ -87,7 +87,8 @@ __global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict_
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = sum;
+    // pip's chain always holds at least one pip_buf: zero segments == one empty segment
+    if (threadIdx.x == 0) *out = nseg ? sum : fold16(sum);
 }
 
 }  // namespace pipck

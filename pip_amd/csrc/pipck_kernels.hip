@@ -53,7 +53,7 @@ __global__ void k_flows6(const pipck_flow6* __restrict__ f, uint32_t n, uint32_t
 // ---------------------------------------------------------------------------
 // fixed-stride kernel
 // ---------------------------------------------------------------------------
-template <int G, int NL, bool VERIFY>
+template <int G, int NL, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
                                                uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
 #pragma unroll
             for (int k = 0; k < NL; k++) {
                 const int c = cb + k * G + sub;
-                v[k] = c < nch ? load_stream(base + c) : u32x4{0u, 0u, 0u, 0u};
+                v[k] = c < nch ? (NT ? load_stream(base + c) : load_plain(base + c)) : u32x4{0u, 0u, 0u, 0u};
             }
 #pragma unroll
             for (int k = 0; k < NL; k++) {
@@ -129,7 +129,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
     return v;
 }
 
-template <bool FINAL, int U>
+template <bool FINAL, int U, bool NT>
 __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ arena, const pipck_desc* __restrict__ desc,
                                                 uint64_t n, const uint32_t* __restrict__ pseudo,
                                                 uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
                     if (s_pre[w][s + st] <= c) s += st;
                 sx[u] = s;
                 const u32x4* p = reinterpret_cast<const u32x4*>(s_base[w][s]) + (c - s_pre[w][s]);
-                v[u] = c < total ? load_stream(p) : u32x4{0u, 0u, 0u, 0u};
+                v[u] = c < total ? (NT ? load_stream(p) : load_plain(p)) : u32x4{0u, 0u, 0u, 0u};
             }
 #pragma unroll
             for (int u = 0; u < U; u++) {
@@ -225,33 +225,45 @@ __global__ void k_chain_finish(const pipck_desc* __restrict__ segs, const uint64
 // ---------------------------------------------------------------------------
 // launch-shape selection
 // ---------------------------------------------------------------------------
-static std::atomic<uint32_t> g_tune_lanes{0}, g_tune_blocks{0};
+struct Tune {
+    std::atomic<uint32_t> lanes{0}, loads{0}, blocks{0}, flags{0};
+};
+static Tune g_tune;
 
 typedef void (*fixed_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
                          uint64_t, uint16_t*, uint8_t*);
 struct Variant {
     int g, nl;
-    fixed_fn sum, verify;
+    fixed_fn fn[2][2];  // [verify][nt]
 };
-#define PIPCK_V(G, NL) {G, NL, k_fixed<G, NL, false>, k_fixed<G, NL, true>}
+#define PIPCK_V(G, NL)                                                               \
+    {                                                                                \
+        G, NL, {                                                                     \
+            {k_fixed<G, NL, false, false>, k_fixed<G, NL, false, true>},             \
+            {k_fixed<G, NL, true, false>, k_fixed<G, NL, true, true>}                \
+        }                                                                            \
+    }
 static const Variant kVariants[] = {
     PIPCK_V(1, 1),  PIPCK_V(1, 2),  PIPCK_V(2, 1),  PIPCK_V(2, 2),  PIPCK_V(4, 1),  PIPCK_V(4, 2),
     PIPCK_V(4, 4),  PIPCK_V(8, 2),  PIPCK_V(8, 4),  PIPCK_V(16, 2), PIPCK_V(16, 4), PIPCK_V(16, 6),
     PIPCK_V(32, 3), PIPCK_V(32, 4), PIPCK_V(64, 2), PIPCK_V(64, 4), PIPCK_V(64, 6), PIPCK_V(64, 9),
 };
 #undef PIPCK_V
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-// Pick the shape that wastes the fewest 16-byte lane slots, then the one with
-// the most loads in flight per lane, then the widest group.
+// A packet should be covered in ONE pass (all its loads in flight at once):
+// among single-pass shapes take the one wasting the fewest 16-byte lane slots,
+// then the most loads in flight per lane, then the widest group.  Packets too
+// long for any single pass use the widest, deepest shape (fewest passes).
 static const Variant& pick_variant(uint32_t nch) {
-    const uint32_t forced = g_tune_lanes.load();
+    const uint32_t fl = g_tune.lanes.load(), fn = g_tune.loads.load();
     const Variant* best = nullptr;
     double best_u = -1.0;
     for (const Variant& v : kVariants) {
-        if (forced && (uint32_t)v.g != forced) continue;
+        if ((fl && (uint32_t)v.g != fl) || (fn && (uint32_t)v.nl != fn)) continue;
         const uint32_t per = (uint32_t)(v.g * v.nl);
-        const uint32_t passes = nch ? (nch + per - 1) / per : 1;
-        const double u = nch ? (double)nch / (double)(per * passes) : 1.0;
+        if (nch > per) continue;
+        const double u = nch ? (double)nch / (double)per : 1.0;
         const bool better = !best || u > best_u + 0.01 ||
                             (u > best_u - 0.01 && (v.nl > best->nl || (v.nl == best->nl && v.g > best->g)));
         if (better) {
@@ -259,12 +271,20 @@ static const Variant& pick_variant(uint32_t nch) {
             best_u = u;
         }
     }
-    return best ? *best : kVariants[sizeof(kVariants) / sizeof(kVariants[0]) - 1];
+    if (best) return *best;
+    for (int i = kNumVariants - 1; i >= 0; i--) {  // multi-pass: deepest matching shape
+        const Variant& v = kVariants[i];
+        if ((fl && (uint32_t)v.g != fl) || (fn && (uint32_t)v.nl != fn)) continue;
+        if (!best || v.g * v.nl > best->g * best->nl) best = &v;
+    }
+    return best ? *best : kVariants[kNumVariants - 1];
 }
+
+static bool use_nt() { return (g_tune.flags.load() & 1u) == 0; }  // bit 0: plain (cached) loads
 
 static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n) {
     uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
-    uint64_t cap = g_tune_blocks.load();
+    uint64_t cap = g_tune.blocks.load();
     if (!cap) cap = (uint64_t)device_cus() * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU
     if (need > cap) need = cap;
     return (uint32_t)(need ? need : 1);
@@ -294,26 +314,35 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;
     const Variant& v = pick_variant(nch);
     const uint32_t grid = grid_for(256 / v.g, n);
-    fixed_fn fn = verify ? v.verify : v.sum;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena, stride, len, n,
-                       d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
+    hipLaunchKernelGGL(v.fn[verify][use_nt()], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
+                       stride, len, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
     PIPCK_LAUNCHED("k_fixed");
     return PIPCK_OK;
 }
 
-constexpr int kRaggedU = 4;
+template <int U>
+static void launch_ragged_u(bool final_, bool nt, dim3 grid, hipStream_t s, const uint8_t* a, const pipck_desc* d,
+                            uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint32_t* err) {
+    if (final_) {
+        if (nt) hipLaunchKernelGGL((k_ragged<true, U, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        else hipLaunchKernelGGL((k_ragged<true, U, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+    } else {
+        if (nt) hipLaunchKernelGGL((k_ragged<false, U, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        else hipLaunchKernelGGL((k_ragged<false, U, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+    }
+}
 
 static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_desc, uint64_t n,
                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint32_t* d_err,
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
-    const uint32_t grid = grid_for(4, tiles);
-    if (final_)
-        hipLaunchKernelGGL((k_ragged<true, kRaggedU>), dim3(grid), dim3(256), 0, s, (const uint8_t*)d_arena, d_desc, n,
-                           d_pseudo, d_out, d_fseg, d_err);
-    else
-        hipLaunchKernelGGL((k_ragged<false, kRaggedU>), dim3(grid), dim3(256), 0, s, (const uint8_t*)d_arena, d_desc,
-                           n, d_pseudo, d_out, d_fseg, d_err);
+    const dim3 grid(grid_for(4, tiles));
+    const uint32_t u = g_tune.loads.load();
+    const bool nt = use_nt();
+    const uint8_t* a = (const uint8_t*)d_arena;
+    if (u == 2) launch_ragged_u<2>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
+    else if (u == 8) launch_ragged_u<8>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
+    else launch_ragged_u<4>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
     PIPCK_LAUNCHED("k_ragged");
     return PIPCK_OK;
 }
@@ -329,9 +358,11 @@ extern "C" {
 
 uint32_t pipck_version(void) { return (1u << 16) | 0u; }
 
-void pipck_tune(uint32_t lanes_per_packet, uint32_t blocks) {
-    g_tune_lanes.store(lanes_per_packet);
-    g_tune_blocks.store(blocks);
+void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags) {
+    g_tune.lanes.store(lanes_per_packet);
+    g_tune.loads.store(loads_per_lane);
+    g_tune.blocks.store(blocks);
+    g_tune.flags.store(flags);
 }
 
 int pipck_flows4_prepare(const pipck_flow4* d_flows, uint32_t n, uint32_t* d_pseudo, void* stream) {

@@ -80,6 +80,9 @@ def kat_cases(rng: random.Random) -> list[dict]:
               "src": v6(1).hex(), "dst": v6(2).hex()})
     C.append({"fn": "inet_chain", "segs": [hx(b"\x01\x02\x03"), hx(b"\x04\x05\x06")], "proto": 6,
               "src": ip("192.168.33.2").hex(), "dst": ip("192.168.33.1").hex()})
+    for fam_fn, w in (("inet_chain", 4), ("inet6_chain", 16)):  # a chain of one empty pip_buf
+        C.append({"fn": fam_fn, "segs": [], "proto": 17, "src": (b"\x6c\x54\x38\x75" * 4)[:w].hex(),
+                  "dst": (b"\x08\xdc\xf0\x38" * 4)[:w].hex()})
     C.append({"fn": "inet", "data": hx(bytes.fromhex("010203040506")), "proto": 6,
               "src": ip("192.168.33.2").hex(), "dst": ip("192.168.33.1").hex()})
     # UDP datagrams of pip_udp.cpp:28-65 shape: 8-B header (uh_sum 0) + (i*13+1) payload

@@ -31,7 +31,7 @@ def gpu():
     assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
     engine.require_gpu()
     yield
-    engine.tune(0, 0)
+    engine.tune()
     torch.cuda.synchronize()
 
 
@@ -160,7 +160,7 @@ LENGTHS = [0, 1, 2, 3, 15, 16, 17, 20, 31, 33, 64, 100, 1023, 1024, 1025, 1480, 
 @pytest.mark.parametrize("lanes", [0, 1, 2, 4, 8, 16, 32, 64])
 def test_fixed_every_shape_vs_oracle(oracle, lanes):
     rng = np.random.default_rng(100 + lanes)
-    engine.tune(lanes, 0)
+    engine.tune(lanes)
     try:
         for length in LENGTHS:
             for fam in (0, 4, 6):
@@ -181,7 +181,7 @@ def test_fixed_every_shape_vs_oracle(oracle, lanes):
                 assert np.array_equal(got, want), (lanes, length, stride, fam, misalign,
                                                    np.nonzero(got != want)[0][:5])
     finally:
-        engine.tune(0, 0)
+        engine.tune()
 
 
 def test_fixed_grid_stride_loop(oracle):
@@ -192,11 +192,11 @@ def test_fixed_grid_stride_loop(oracle):
     _, pseudo = engine.gen_flows(4, N_FLOWS, 77, 6)
     want = oracle.batch_fixed(host, 1488, 1480, 5000, 4, 6, 77, N_FLOWS, 123)
     for blocks in (1, 3, 17):
-        engine.tune(0, blocks)
+        engine.tune(blocks=blocks)
         try:
             got = u16(engine.checksum_fixed(arena, 1488, 1480, 5000, pseudo, N_FLOWS, None, 123))
         finally:
-            engine.tune(0, 0)
+            engine.tune()
         assert np.array_equal(got, want), blocks
 
 

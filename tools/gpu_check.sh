@@ -22,10 +22,12 @@ for s in $STEPS; do
     bench)  timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$? ;;
     prof)   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
               python3 bench.py --steps 20 --warmup 5 --no-cpu > "$OUT/prof_bench.json" 2> "$OUT/prof.err"; rc=$? ;;
+    sweep)  timeout -k 10 900 python3 tools/sweep.py ${SWEEP_ARGS:-} > "$OUT/sweep.jsonl" 2> "$OUT/sweep.err"; rc=$? ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   echo "   rc=$rc"
-  tail -3 "$OUT/$( [ "$s" = pytest ] && echo pytest_gpu.log || ([ "$s" = smoke ] && echo smoke.log || ([ "$s" = bench ] && echo bench.json || echo prof.err)))" 2>/dev/null
+  case "$s" in pytest) f=pytest_gpu.log ;; smoke) f=smoke.log ;; bench) f=bench.json ;; sweep) f=sweep.err ;; *) f=prof.err ;; esac
+  tail -3 "$OUT/$f" 2>/dev/null
   stop_if_fatal "$rc" "$s"
 done
 echo "== done $(date +%T)"
