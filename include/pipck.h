@@ -120,7 +120,7 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
  * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
  * in flight); blocks caps the grid; flags bit 0 = plain (cached) loads instead
- * of non-temporal ones. */
+ * of non-temporal ones, bit 1 = never use the flat-stream fixed kernel. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */

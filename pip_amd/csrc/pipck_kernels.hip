@@ -19,6 +19,7 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <vector>
@@ -109,6 +110,97 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
             flow += flow_step;
             if (flow >= n_flows) flow -= n_flows;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// flat-stream kernel: fixed strides of whole 16-byte chunks, >= 64 chunks each
+// ---------------------------------------------------------------------------
+// A wave owns a run of consecutive packets and streams their chunks as
+// consecutive 1 KiB rows (lane l of row r reads chunk 64r + l): every load
+// instruction is one fully coalesced 1 KiB read, U rows are in flight per
+// wave, and since a packet spans >= 64 chunks a row holds at most one packet
+// boundary.  Lanes keep a running u64 sum for the packet the row is in; at a
+// boundary the finished packet's partials are folded and wave-reduced once.
+__device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    return s;
+}
+
+template <bool VERIFY>
+__device__ __forceinline__ void flat_finish(uint64_t acc, uint64_t pkt, uint32_t flow, const uint32_t* pseudo,
+                                            const uint32_t* flow_of, uint32_t lterm, uint16_t* out, uint8_t* ok,
+                                            int lane) {
+    const uint32_t s = wave_reduce_add(fold64(acc));
+    if (lane == 0) {
+        const uint32_t F = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
+        const uint32_t P = pseudo ? pseudo[flow_of ? flow_of[pkt] : flow] + lterm : 0u;
+        if (VERIFY)
+            ok[pkt] = fold16(P + F) == 0xFFFFu;
+        else
+            out[pkt] = finish(P, F);
+    }
+}
+
+template <int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
+                                              uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                              const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
+    const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
+    const uint32_t lterm = len_term(len);
+    const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
+    const uint64_t n_tasks = (n + run - 1) / run;
+    const uint64_t wstep = (uint64_t)gridDim.x * 4;
+    for (uint64_t task = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); task < n_tasks; task += wstep) {
+        const uint64_t p0 = task * run;
+        const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
+        const uint32_t tchunks = np * cpp;
+        const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
+        uint32_t flow = implicit_flow ? (uint32_t)((flow_origin + p0) % n_flows) : 0u;
+        uint64_t acc = 0;
+        for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
+            u32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rs = r0 + u * 64;  // wave-uniform row start
+                const uint32_t krow = rs % cpp;
+                uint32_t k = krow + lane;
+                if (k >= cpp) k -= cpp;
+                const uint32_t c = rs + lane;
+                v[u] = (c < tchunks && k < nch) ? (NT ? load_stream(tb + c) : load_plain(tb + c))
+                                                 : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rs = r0 + u * 64;
+                if (rs >= tchunks) continue;  // wave-uniform; keeps the loop fully unrolled
+                const uint32_t prow = rs / cpp, krow = rs - prow * cpp;
+                if (krow == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
+                    flat_finish<VERIFY>(acc, p0 + prow - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
+                    if (implicit_flow && ++flow == n_flows) flow = 0;
+                    acc = 0;
+                }
+                uint32_t k = krow + lane;
+                if (k >= cpp) k -= cpp;
+                u32x4 x = v[u];
+                if (k == nch - 1 && tail < 16) x = mask_chunk(x, 0, tail);
+                const uint64_t val = sum4(x);
+                const uint32_t b = cpp - krow;  // first lane holding the next packet
+                if (b >= 64 || prow + 1 >= np) {
+                    acc += val;
+                } else {
+                    acc += lane < (int)b ? val : 0ull;
+                    flat_finish<VERIFY>(acc, p0 + prow, flow, pseudo, flow_of, lterm, out, ok, lane);
+                    if (implicit_flow && ++flow == n_flows) flow = 0;
+                    acc = lane < (int)b ? 0ull : val;
+                }
+            }
+        }
+        flat_finish<VERIFY>(acc, p0 + np - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
     }
 }
 
@@ -280,7 +372,25 @@ static const Variant& pick_variant(uint32_t nch) {
     return best ? *best : kVariants[kNumVariants - 1];
 }
 
-static bool use_nt() { return (g_tune.flags.load() & 1u) == 0; }  // bit 0: plain (cached) loads
+static bool use_nt() { return (g_tune.flags.load() & 1u) == 0; }       // bit 0: plain (cached) loads
+static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
+
+typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*);
+struct FlatVariant {
+    int u;
+    flat_fn fn[2][2];  // [verify][nt]
+};
+#define PIPCK_F(U)                                                                        \
+    {                                                                                     \
+        U, {                                                                              \
+            {k_flat<U, false, false>, k_flat<U, false, true>},                            \
+            {k_flat<U, true, false>, k_flat<U, true, true>}                               \
+        }                                                                                 \
+    }
+static const FlatVariant kFlat[] = {PIPCK_F(2), PIPCK_F(4), PIPCK_F(8), PIPCK_F(16)};
+#undef PIPCK_F
+constexpr int kFlatDefaultU = 8;
 
 static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n) {
     uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
@@ -311,6 +421,23 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         return PIPCK_EINVAL;
     }
     const bool aligned = ((uintptr_t)d_arena % 16 == 0) && (stride % 16 == 0);
+    if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
+        len <= stride) {
+        const uint32_t cpp = (uint32_t)(stride / 16);
+        const uint32_t want_u = g_tune.loads.load() ? g_tune.loads.load() : (uint32_t)kFlatDefaultU;
+        const FlatVariant* fv = &kFlat[0];
+        for (const FlatVariant& f : kFlat)
+            if ((uint32_t)f.u == want_u) fv = &f;
+        // a wave task covers >= ~32 rows of 1 KiB so the row pipeline rarely restarts
+        const uint32_t run = std::max<uint32_t>(1u, (64u * 32u) / cpp);
+        const uint64_t tasks = (n + run - 1) / run;
+        const uint32_t grid = grid_for(4, tasks);
+        hipLaunchKernelGGL(fv->fn[verify][use_nt()], dim3(grid), dim3(256), 0, as_stream(stream),
+                           (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
+                           flow_origin, d_out, d_ok);
+        PIPCK_LAUNCHED("k_flat");
+        return PIPCK_OK;
+    }
     const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;
     const Variant& v = pick_variant(nch);
     const uint32_t grid = grid_for(256 / v.g, n);

@@ -184,6 +184,37 @@ def test_fixed_every_shape_vs_oracle(oracle, lanes):
         engine.tune()
 
 
+@pytest.mark.parametrize("rows", [2, 4, 8, 16])
+@pytest.mark.parametrize("nt", [False, True])
+def test_flat_stream_kernel_vs_oracle(oracle, rows, nt):
+    """The flat-stream fixed kernel (16-byte-multiple strides >= 1 KiB, aligned
+    arena): packet boundaries at every lane position of a row, boundaries that
+    fall exactly on row ends, stride padding wider than a row, runs cut short."""
+    rng = np.random.default_rng(rows * 10 + nt)
+    cases = [(1024, 1024), (1024, 1023), (1024, 0), (1040, 1025), (1488, 1480), (1504, 1480), (2048, 17),
+             (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
+    try:
+        for stride, length in cases:
+            for blocks in (0, 1, 7):
+                engine.tune(0, rows, blocks, plain_loads=not nt)
+                n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
+                host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+                if n > 2:
+                    host[stride:2 * stride] = 0xFF
+                _, arena = upload(host, 0)
+                fam = int(rng.choice([0, 4, 6]))
+                seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
+                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+                got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+                assert np.array_equal(got, want), (stride, length, n, blocks, np.nonzero(got != want)[0][:5])
+                ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
+                # a packet verifies exactly when its recomputed checksum is 0x0000
+                assert np.array_equal(ok.astype(bool), got == 0)
+    finally:
+        engine.tune()
+
+
 def test_fixed_grid_stride_loop(oracle):
     """Force a tiny grid so every block loops over many packets."""
     rng = np.random.default_rng(5)

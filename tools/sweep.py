@@ -59,13 +59,15 @@ def main():
             engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
             nbytes = (w.length + 2) * n
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
-            lanes = [0, 16, 32, 64] if a.quick else [0, 1, 2, 4, 8, 16, 32, 64]
-            blocks = [0, 512, 1024, 4096] if not a.quick else [0, 2048]
+            lanes = [8, 32] if a.quick else [1, 2, 4, 8, 16, 32, 64]
+            blocks = [0, 4096] if a.quick else [0, 1024, 4096]
             shapes = [(g, 0, b, nt) for g, b, nt in itertools.product(lanes, blocks, (False, True))]
+            # the flat-stream kernel (lanes 0 = automatic): rows in flight x grid x load policy
+            shapes += [(0, u, b, nt) for u, b, nt in itertools.product((2, 4, 8, 16), (0, 4096, 8192), (False, True))]
         engine.tune()
         ref = run().clone()
         for g, u, b, nt in shapes:
-            engine.tune(g, u, b, plain_loads=not nt)
+            engine.tune(g, u, b, plain_loads=not nt, flat=(g == 0))
             ms = timed(run, a.iters)
             ok = bool(torch.equal(run(), ref))
             print(json.dumps({"workload": w.name, "lanes": g, "loads": u, "blocks": b, "nt": nt, "ms": round(ms, 4),
