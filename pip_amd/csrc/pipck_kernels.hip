@@ -143,7 +143,68 @@ __device__ __forceinline__ void flat_finish(uint64_t acc, uint64_t pkt, uint32_t
     }
 }
 
-template <int U, bool VERIFY, bool NT>
+// Row bookkeeping is incremental (cpp >= 64, so a row advances the packet by at
+// most one): no divisions in the loop.  PIPE issues the next U rows' loads
+// before reducing the current U, so a wave never drains its memory queue.
+struct RowPos {
+    uint32_t pkt, k;  // packet (within the task) and chunk-in-packet at lane 0 of the row
+    __device__ __forceinline__ void advance(uint32_t cpp) {
+        k += 64;
+        if (k >= cpp) {
+            k -= cpp;
+            pkt++;
+        }
+    }
+};
+
+template <int U, bool NT>
+__device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], const u32x4* tb, uint32_t r0, uint32_t tchunks,
+                                               RowPos& lp, uint32_t cpp, uint32_t nch, int lane) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        uint32_t k = lp.k + lane;
+        if (k >= cpp) k -= cpp;
+        const uint32_t c = r0 + u * 64 + lane;
+        v[u] = (c < tchunks && k < nch) ? (NT ? load_stream(tb + c) : load_plain(tb + c)) : u32x4{0u, 0u, 0u, 0u};
+        lp.advance(cpp);
+    }
+}
+
+template <int U, bool VERIFY>
+__device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r0, uint32_t tchunks, RowPos& pp,
+                                                 uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
+                                                 uint64_t p0, uint32_t& flow, bool implicit_flow, uint32_t n_flows,
+                                                 const uint32_t* pseudo, const uint32_t* flow_of, uint32_t lterm,
+                                                 uint16_t* out, uint8_t* ok, int lane) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t rs = r0 + u * 64;  // wave-uniform
+        if (rs < tchunks) {
+            if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
+                flat_finish<VERIFY>(acc, p0 + pp.pkt - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
+                if (implicit_flow && ++flow == n_flows) flow = 0;
+                acc = 0;
+            }
+            uint32_t k = pp.k + lane;
+            if (k >= cpp) k -= cpp;
+            u32x4 x = v[u];
+            if (k == nch - 1 && tail < 16) x = mask_chunk(x, 0, tail);
+            const uint64_t val = sum4(x);
+            const uint32_t b = cpp - pp.k;  // first lane holding the next packet
+            if (b >= 64 || pp.pkt + 1 >= np) {
+                acc += val;
+            } else {
+                acc += lane < (int)b ? val : 0ull;
+                flat_finish<VERIFY>(acc, p0 + pp.pkt, flow, pseudo, flow_of, lterm, out, ok, lane);
+                if (implicit_flow && ++flow == n_flows) flow = 0;
+                acc = lane < (int)b ? 0ull : val;
+            }
+        }
+        pp.advance(cpp);
+    }
+}
+
+template <int U, bool PIPE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
                                               uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
@@ -162,42 +223,24 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena,
         const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
         uint32_t flow = implicit_flow ? (uint32_t)((flow_origin + p0) % n_flows) : 0u;
         uint64_t acc = 0;
+        RowPos lp{0, 0}, pp{0, 0};
+        u32x4 v[U];
+        flat_load_rows<U, NT>(v, tb, 0, tchunks, lp, cpp, nch, lane);
         for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
-            u32x4 v[U];
+            if (PIPE) {
+                u32x4 nx[U];
+                const bool more = r0 + 64 * U < tchunks;  // wave-uniform
+                if (more) flat_load_rows<U, NT>(nx, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
+                flat_reduce_rows<U, VERIFY>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, p0, flow, implicit_flow,
+                                            n_flows, pseudo, flow_of, lterm, out, ok, lane);
+                if (more) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t rs = r0 + u * 64;  // wave-uniform row start
-                const uint32_t krow = rs % cpp;
-                uint32_t k = krow + lane;
-                if (k >= cpp) k -= cpp;
-                const uint32_t c = rs + lane;
-                v[u] = (c < tchunks && k < nch) ? (NT ? load_stream(tb + c) : load_plain(tb + c))
-                                                 : u32x4{0u, 0u, 0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t rs = r0 + u * 64;
-                if (rs >= tchunks) continue;  // wave-uniform; keeps the loop fully unrolled
-                const uint32_t prow = rs / cpp, krow = rs - prow * cpp;
-                if (krow == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
-                    flat_finish<VERIFY>(acc, p0 + prow - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
-                    if (implicit_flow && ++flow == n_flows) flow = 0;
-                    acc = 0;
+                    for (int u = 0; u < U; u++) v[u] = nx[u];
                 }
-                uint32_t k = krow + lane;
-                if (k >= cpp) k -= cpp;
-                u32x4 x = v[u];
-                if (k == nch - 1 && tail < 16) x = mask_chunk(x, 0, tail);
-                const uint64_t val = sum4(x);
-                const uint32_t b = cpp - krow;  // first lane holding the next packet
-                if (b >= 64 || prow + 1 >= np) {
-                    acc += val;
-                } else {
-                    acc += lane < (int)b ? val : 0ull;
-                    flat_finish<VERIFY>(acc, p0 + prow, flow, pseudo, flow_of, lterm, out, ok, lane);
-                    if (implicit_flow && ++flow == n_flows) flow = 0;
-                    acc = lane < (int)b ? 0ull : val;
-                }
+            } else {
+                flat_reduce_rows<U, VERIFY>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, p0, flow, implicit_flow,
+                                            n_flows, pseudo, flow_of, lterm, out, ok, lane);
+                if (r0 + 64 * U < tchunks) flat_load_rows<U, NT>(v, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
             }
         }
         flat_finish<VERIFY>(acc, p0 + np - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
@@ -379,18 +422,31 @@ typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, 
                         const uint32_t*, uint64_t, uint16_t*, uint8_t*);
 struct FlatVariant {
     int u;
+    bool pipe;
     flat_fn fn[2][2];  // [verify][nt]
 };
-#define PIPCK_F(U)                                                                        \
+#define PIPCK_F(U, P)                                                                     \
     {                                                                                     \
-        U, {                                                                              \
-            {k_flat<U, false, false>, k_flat<U, false, true>},                            \
-            {k_flat<U, true, false>, k_flat<U, true, true>}                               \
+        U, P, {                                                                           \
+            {k_flat<U, P, false, false>, k_flat<U, P, false, true>},                      \
+            {k_flat<U, P, true, false>, k_flat<U, P, true, true>}                         \
         }                                                                                 \
     }
-static const FlatVariant kFlat[] = {PIPCK_F(2), PIPCK_F(4), PIPCK_F(8), PIPCK_F(16)};
+// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9 = pipelined U = 2/4/8
+static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_F(8, false), PIPCK_F(16, false),
+                                    PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true)};
 #undef PIPCK_F
-constexpr int kFlatDefaultU = 8;
+static const FlatVariant& flat_variant(uint32_t loads) {
+    switch (loads) {
+        case 2: return kFlat[0];
+        case 4: return kFlat[1];
+        case 8: return kFlat[2];
+        case 3: return kFlat[4];
+        case 5: return kFlat[5];
+        case 9: return kFlat[6];
+        default: return kFlat[3];  // 16 rows in flight
+    }
+}
 
 static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n) {
     uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
@@ -424,10 +480,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        const uint32_t want_u = g_tune.loads.load() ? g_tune.loads.load() : (uint32_t)kFlatDefaultU;
-        const FlatVariant* fv = &kFlat[0];
-        for (const FlatVariant& f : kFlat)
-            if ((uint32_t)f.u == want_u) fv = &f;
+        const FlatVariant* fv = &flat_variant(g_tune.loads.load());
         // a wave task covers >= ~32 rows of 1 KiB so the row pipeline rarely restarts
         const uint32_t run = std::max<uint32_t>(1u, (64u * 32u) / cpp);
         const uint64_t tasks = (n + run - 1) / run;

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--workloads", default="cfg5,cfg2,cfg3,cfg4,cfg1")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--flat-only", action="store_true")
     a = ap.parse_args()
     engine.require_gpu()
     for name in a.workloads.split(","):
@@ -61,9 +62,10 @@ def main():
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             lanes = [8, 32] if a.quick else [1, 2, 4, 8, 16, 32, 64]
             blocks = [0, 4096] if a.quick else [0, 1024, 4096]
-            shapes = [(g, 0, b, nt) for g, b, nt in itertools.product(lanes, blocks, (False, True))]
-            # the flat-stream kernel (lanes 0 = automatic): rows in flight x grid x load policy
-            shapes += [(0, u, b, nt) for u, b, nt in itertools.product((2, 4, 8, 16), (0, 4096, 8192), (False, True))]
+            shapes = [] if a.flat_only else [(g, 0, b, nt) for g, b, nt in itertools.product(lanes, blocks, (False, True))]
+            # the flat-stream kernel (lanes 0 = automatic): rows in flight (3/5/9 = pipelined 2/4/8) x grid x policy
+            shapes += [(0, u, b, nt) for u, b, nt in itertools.product((4, 8, 16, 3, 5, 9), (0, 4096, 8192, 16384),
+                                                                       (False, True))]
         engine.tune()
         ref = run().clone()
         for g, u, b, nt in shapes:
