@@ -119,8 +119,10 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
 /* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
  * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
- * in flight); blocks caps the grid; flags bit 0 = plain (cached) loads instead
- * of non-temporal ones, bit 1 = never use the flat-stream fixed kernel. */
+ * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9 = pipelined
+ * 2/4/8); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
+ * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
+ * fixed kernel, bits 8.. = 1 KiB rows per flat-kernel wave task (default 32). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */

@@ -415,7 +415,6 @@ static const Variant& pick_variant(uint32_t nch) {
     return best ? *best : kVariants[kNumVariants - 1];
 }
 
-static bool use_nt() { return (g_tune.flags.load() & 1u) == 0; }       // bit 0: plain (cached) loads
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
@@ -444,16 +443,29 @@ static const FlatVariant& flat_variant(uint32_t loads) {
         case 3: return kFlat[4];
         case 5: return kFlat[5];
         case 9: return kFlat[6];
-        default: return kFlat[3];  // 16 rows in flight
+        case 16: return kFlat[3];
+        default: return kFlat[2];
     }
 }
 
-static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n) {
+// Default grid: blocks_per_cu 256-thread blocks per CU (more than are resident
+// at once: blocks that finish early are replaced, which balances the tail).
+static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n, uint32_t blocks_per_cu = 8) {
     uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
     uint64_t cap = g_tune.blocks.load();
-    if (!cap) cap = (uint64_t)device_cus() * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU
+    if (!cap) cap = (uint64_t)device_cus() * blocks_per_cu;
     if (need > cap) need = cap;
     return (uint32_t)(need ? need : 1);
+}
+
+// Load policy: tune flags bit 0 forces plain loads, bit 2 forces non-temporal
+// ones; otherwise each kernel uses what measured faster on MI355X
+// (profiles/README.md): nt for the streaming kernels, plain for small groups.
+static bool nt_for(bool streaming) {
+    const uint32_t f = g_tune.flags.load();
+    if (f & 1u) return false;
+    if (f & 4u) return true;
+    return streaming;
 }
 
 static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
@@ -480,12 +492,15 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        const FlatVariant* fv = &flat_variant(g_tune.loads.load());
+        // rows in flight per wave: 16 for jumbo packets, 8 below 4 KiB (measured, profiles/README.md)
+        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (cpp >= 256 ? 16u : 8u);
+        const FlatVariant* fv = &flat_variant(loads);
         // a wave task covers >= ~32 rows of 1 KiB so the row pipeline rarely restarts
-        const uint32_t run = std::max<uint32_t>(1u, (64u * 32u) / cpp);
+        const uint32_t rows = (g_tune.flags.load() >> 8) ? (g_tune.flags.load() >> 8) : 32u;
+        const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
-        const uint32_t grid = grid_for(4, tasks);
-        hipLaunchKernelGGL(fv->fn[verify][use_nt()], dim3(grid), dim3(256), 0, as_stream(stream),
+        const uint32_t grid = grid_for(4, tasks, 64);
+        hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), 0, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok);
         PIPCK_LAUNCHED("k_flat");
@@ -494,7 +509,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;
     const Variant& v = pick_variant(nch);
     const uint32_t grid = grid_for(256 / v.g, n);
-    hipLaunchKernelGGL(v.fn[verify][use_nt()], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
+    hipLaunchKernelGGL(v.fn[verify][nt_for(false)], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
                        stride, len, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
     PIPCK_LAUNCHED("k_fixed");
     return PIPCK_OK;
@@ -518,7 +533,7 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
     const uint64_t tiles = (n + 63) / 64;
     const dim3 grid(grid_for(4, tiles));
     const uint32_t u = g_tune.loads.load();
-    const bool nt = use_nt();
+    const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     if (u == 2) launch_ragged_u<2>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
     else if (u == 8) launch_ragged_u<8>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);

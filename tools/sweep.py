@@ -64,15 +64,18 @@ def main():
             blocks = [0, 4096] if a.quick else [0, 1024, 4096]
             shapes = [] if a.flat_only else [(g, 0, b, nt) for g, b, nt in itertools.product(lanes, blocks, (False, True))]
             # the flat-stream kernel (lanes 0 = automatic): rows in flight (3/5/9 = pipelined 2/4/8) x grid x policy
-            shapes += [(0, u, b, nt) for u, b, nt in itertools.product((4, 8, 16, 3, 5, 9), (0, 4096, 8192, 16384),
-                                                                       (False, True))]
+            shapes += [(0, u, b, nt) for u, b, nt in itertools.product((8, 16, 9), (0, 16384, 32768), (False, True))]
+            shapes += [(0, u, 0, True, r) for u in (8, 16) for r in (16, 64, 128, 256)]
         engine.tune()
         ref = run().clone()
-        for g, u, b, nt in shapes:
-            engine.tune(g, u, b, plain_loads=not nt, flat=(g == 0))
+        for shape in shapes:
+            g, u, b, nt = shape[:4]
+            rows = shape[4] if len(shape) > 4 else 0
+            engine.tune(g, u, b, plain_loads=not nt, nt_loads=nt, flat=(g == 0), rows_per_task=rows)
             ms = timed(run, a.iters)
             ok = bool(torch.equal(run(), ref))
-            print(json.dumps({"workload": w.name, "lanes": g, "loads": u, "blocks": b, "nt": nt, "ms": round(ms, 4),
+            print(json.dumps({"workload": w.name, "lanes": g, "loads": u, "blocks": b, "nt": nt, "rows": rows,
+                              "ms": round(ms, 4),
                               "GBps": round(nbytes / ms / 1e6, 1), "ok": ok}), flush=True)
         engine.tune()
         del arena
