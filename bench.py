@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--packets-per-gpu", type=int, default=0, help="override the per-GPU shard size")
     p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and host end-to-end legs")
-    p.add_argument("--traffic", default="", help="JSON file with PMC-measured HBM bytes per launch")
+    p.add_argument("--traffic", default="auto",
+                   help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json)")
     return p.parse_args()
 
 
@@ -117,8 +118,12 @@ def main() -> int:
     algo_bytes = l4_bytes + 2 * count  # per launch on this rank
     achieved = algo_bytes / launch_s / 1e9
     traffic = None
-    if args.traffic and Path(args.traffic).exists():
-        traffic = json.loads(Path(args.traffic).read_text()).get("hbm_bytes_per_launch")
+    tpath = Path(args.traffic) if args.traffic != "auto" else ROOT / "profiles" / f"traffic_cfg{w.cfg}.json"
+    if args.traffic and tpath.exists():
+        t = json.loads(tpath.read_text())
+        # only valid for the launch it was measured on: same kernel shape and per-launch byte count
+        if t.get("algorithmic_bytes_per_launch") == algo_bytes:
+            traffic = t.get("hbm_bytes_per_launch")
 
     line = {
         "metric": METRIC,

@@ -495,8 +495,9 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // rows in flight per wave: 16 for jumbo packets, 8 below 4 KiB (measured, profiles/README.md)
         const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (cpp >= 256 ? 16u : 8u);
         const FlatVariant* fv = &flat_variant(loads);
-        // a wave task covers >= ~32 rows of 1 KiB so the row pipeline rarely restarts
-        const uint32_t rows = (g_tune.flags.load() >> 8) ? (g_tune.flags.load() >> 8) : 32u;
+        // a wave task covers ~128 rows of 1 KiB (measured best for 1.5-9 KiB packets):
+        // the row pipeline rarely restarts and consecutive waves stream adjacent 128 KiB spans
+        const uint32_t rows = (g_tune.flags.load() >> 8) ? (g_tune.flags.load() >> 8) : 128u;
         const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 64);
