@@ -69,7 +69,8 @@ def main() -> int:
 
     from pip_amd import engine
 
-    torch.cuda.set_device(env.local_rank)
+    # one GPU per rank; ranks beyond the visible devices share them (rehearsing N>1 on a 1-GPU box)
+    torch.cuda.set_device(env.local_rank % max(1, torch.cuda.device_count()))
     engine.require_gpu()
     w = ALL[args.workload] if args.workload in ALL else BY_CFG[int(args.workload.lstrip("cfg"))]
     per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
