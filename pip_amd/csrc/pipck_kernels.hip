@@ -255,81 +255,130 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
+// Inclusive wave-64 prefix sum on the DPP crossbar (GFX9 DPP: row_shr inside
+// 16-lane rows, then row_bcast:15 / row_bcast:31 across rows) -- no LDS trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
 }
 
-template <bool FINAL, int U, bool NT>
+struct RaggedTileLds {
+    uint32_t pre[64];   // exclusive chunk prefix of the tile's segments
+    uint32_t acc[64];   // LE residue partial per segment
+    uint32_t span[64];  // (end << 4) | head, relative to the 16-byte-aligned base
+    uint64_t base[64];  // 16-byte-aligned base address of each segment
+};
+
+// Map U rows of the tile's chunk stream to segments (binary search over the
+// chunk prefix: the last segment starting at or before the chunk, which skips
+// empty segments) and issue their 16-byte loads.
+template <int U, bool NT>
+__device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
+                                             u32x4 (&v)[U], uint32_t (&sx)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t c = c0 + u * 64 + lane;
+        uint32_t s = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+            if (t.pre[s + st] <= c) s += st;
+        sx[u] = s;
+        const u32x4* p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
+        v[u] = c < total ? (NT ? load_stream(p) : load_plain(p)) : u32x4{0u, 0u, 0u, 0u};
+    }
+}
+
+// Reduce U rows by segment: a wave prefix scan per row; the lane holding a
+// segment's last chunk in the row adds (its prefix - the prefix just before
+// the segment's first chunk in the row) to the segment's LDS partial.
+template <int U>
+__device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
+                                              const u32x4 (&v)[U], const uint32_t (&sx)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t row = c0 + u * 64;
+        if (row >= total) continue;  // wave-uniform
+        const uint32_t c = row + lane;
+        const bool active = c < total;
+        const uint32_t s = sx[u];
+        const uint32_t pre = t.pre[s];
+        const uint32_t span = t.span[s];
+        const int rel = (int)(c - pre);
+        const int lo = rel == 0 ? (int)(span & 15) : 0;
+        const int hi = (int)(span >> 4) - 16 * rel;
+        u32x4 x = v[u];
+        if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+        const uint32_t val = active ? fold64(sum4(x)) : 0u;
+        const uint32_t inc = wave_incl_scan(val);
+        const bool last_chunk = hi <= 16;  // this chunk ends its segment
+        const bool tail = active && (lane == 63 || last_chunk);
+        const int head_lane = (int)pre - (int)row;  // lane of the segment's first chunk in this row
+        const uint32_t before = __shfl(inc, max(head_lane, 1) - 1, 64);
+        if (tail) atomicAdd(&t.acc[s], inc - (head_lane > 0 ? before : 0u));
+    }
+}
+
+template <bool FINAL, int U, bool PIPE, bool NT>
 __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ arena, const pipck_desc* __restrict__ desc,
                                                 uint64_t n, const uint32_t* __restrict__ pseudo,
                                                 uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
                                                 uint32_t* __restrict__ err) {
-    __shared__ uint32_t s_pre[4][64];   // exclusive chunk prefix of the tile's segments
-    __shared__ uint32_t s_acc[4][64];   // LE residue partial per segment
-    __shared__ uint32_t s_span[4][64];  // (end << 4) | head, relative to the aligned base
-    __shared__ uint64_t s_base[4][64];  // 16-byte-aligned base address of each segment
+    __shared__ RaggedTileLds s_tile[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    RaggedTileLds& t = s_tile[w];
     const uint64_t tstep = (uint64_t)gridDim.x * 4;
-    for (uint64_t tile = (uint64_t)blockIdx.x * 4 + w; tile * 64 < n; tile += tstep) {
+    uint64_t tile = (uint64_t)blockIdx.x * 4 + w;
+    pipck_desc dn = pipck_desc{0, 0, 0};
+    if (tile * 64 + lane < n) dn = desc[tile * 64 + lane];
+    for (; tile * 64 < n; tile += tstep) {
         const uint64_t seg = tile * 64 + lane;
         const bool valid = seg < n;
-        pipck_desc d = valid ? desc[seg] : pipck_desc{0, 0, 0};
-        const bool bad = d.len > PIPCK_MAX_SEG_LEN;
-        const uint32_t len = bad ? 0u : d.len;
+        const pipck_desc d = dn;
+        // prefetch the next tile's descriptors; they land while this tile streams
+        const uint64_t nseg = (tile + tstep) * 64 + lane;
+        if ((tile + tstep) * 64 < n) dn = nseg < n ? desc[nseg] : pipck_desc{0, 0, 0};
+        const bool bad = valid && d.len > PIPCK_MAX_SEG_LEN;
+        const uint32_t len = (valid && !bad) ? d.len : 0u;
         const uintptr_t addr = (uintptr_t)arena + d.offset;
         const uint32_t head = (uint32_t)(addr & 15);
         const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
-        const uint32_t incl = wave_incl_scan(nch, lane);
+        const uint32_t incl = wave_incl_scan(nch);
         const uint32_t total = __shfl(incl, 63, 64);
-        s_pre[w][lane] = incl - nch;
-        s_span[w][lane] = ((head + len) << 4) | head;
-        s_base[w][lane] = addr - head;
-        s_acc[w][lane] = 0;
+        t.pre[lane] = incl - nch;
+        t.span[lane] = ((head + len) << 4) | head;
+        t.base[lane] = addr - head;
+        t.acc[lane] = 0;
         wave_sync();
+        u32x4 v[U];
+        uint32_t sx[U];
+        if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx);
         for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
-            u32x4 v[U];
-            uint32_t sx[U];
+            const bool more = c0 + 64 * U < total;  // wave-uniform
+            if (PIPE) {
+                u32x4 nv[U];
+                uint32_t nsx[U];
+                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx);
+                ragged_reduce<U>(t, c0, total, lane, v, sx);
+                if (more) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t c = c0 + u * 64 + lane;
-                uint32_t s = 0;  // last segment whose first chunk is <= c (skips empty segments)
-#pragma unroll
-                for (int st = 32; st > 0; st >>= 1)
-                    if (s_pre[w][s + st] <= c) s += st;
-                sx[u] = s;
-                const u32x4* p = reinterpret_cast<const u32x4*>(s_base[w][s]) + (c - s_pre[w][s]);
-                v[u] = c < total ? (NT ? load_stream(p) : load_plain(p)) : u32x4{0u, 0u, 0u, 0u};
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t row = c0 + u * 64;
-                const uint32_t c = row + lane;
-                const bool active = c < total;
-                const uint32_t s = sx[u];
-                const uint32_t pre = s_pre[w][s];
-                const uint32_t span = s_span[w][s];
-                const int rel = (int)(c - pre);
-                const int lo = rel == 0 ? (int)(span & 15) : 0;
-                const int hi = (int)(span >> 4) - 16 * rel;
-                u32x4 x = v[u];
-                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
-                const uint32_t val = active ? fold64(sum4(x)) : 0u;
-                const uint32_t inc = wave_incl_scan(val, lane);
-                const uint32_t s_next = __shfl_down(s, 1, 64);
-                const bool tail = active && (lane == 63 || c + 1 >= total || s_next != s);
-                const int head_lane = (int)pre - (int)row;  // lane holding the segment's first chunk in this row
-                const uint32_t before = __shfl(inc, max(head_lane, 1) - 1, 64);
-                if (tail) atomicAdd(&s_acc[w][s], inc - (head_lane > 0 ? before : 0u));
+                    for (int u = 0; u < U; u++) {
+                        v[u] = nv[u];
+                        sx[u] = nsx[u];
+                    }
+                }
+            } else {
+                ragged_reduce<U>(t, c0, total, lane, v, sx);
+                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx);
             }
         }
         wave_sync();
         if (valid) {
-            const uint32_t F = bad ? 0u : be_fold(s_acc[w][lane], addr);
+            const uint32_t F = bad ? 0u : be_fold(t.acc[lane], addr);
             if (FINAL) {
                 const uint32_t P = pseudo ? pseudo[d.flow] + len_term(len) : 0u;
                 out[seg] = bad ? (uint16_t)0 : finish(P, F);
@@ -516,15 +565,15 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     return PIPCK_OK;
 }
 
-template <int U>
+template <int U, bool PIPE>
 static void launch_ragged_u(bool final_, bool nt, dim3 grid, hipStream_t s, const uint8_t* a, const pipck_desc* d,
                             uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint32_t* err) {
     if (final_) {
-        if (nt) hipLaunchKernelGGL((k_ragged<true, U, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
-        else hipLaunchKernelGGL((k_ragged<true, U, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        if (nt) hipLaunchKernelGGL((k_ragged<true, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        else hipLaunchKernelGGL((k_ragged<true, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
     } else {
-        if (nt) hipLaunchKernelGGL((k_ragged<false, U, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
-        else hipLaunchKernelGGL((k_ragged<false, U, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        if (nt) hipLaunchKernelGGL((k_ragged<false, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
+        else hipLaunchKernelGGL((k_ragged<false, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err);
     }
 }
 
@@ -533,12 +582,18 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
     const dim3 grid(grid_for(4, tiles));
-    const uint32_t u = g_tune.loads.load();
+    // loads_per_lane: 2/4/8 rows in flight, 3/5/9 = pipelined 2/4/8 (default: pipelined 4)
+    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 5u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
-    if (u == 2) launch_ragged_u<2>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
-    else if (u == 8) launch_ragged_u<8>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
-    else launch_ragged_u<4>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err);
+    switch (u) {
+        case 2: launch_ragged_u<2, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        case 4: launch_ragged_u<4, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        case 8: launch_ragged_u<8, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        case 3: launch_ragged_u<2, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        case 9: launch_ragged_u<8, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        default: launch_ragged_u<4, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+    }
     PIPCK_LAUNCHED("k_ragged");
     return PIPCK_OK;
 }
