@@ -581,9 +581,11 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint32_t* d_err,
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
-    const dim3 grid(grid_for(4, tiles));
-    // loads_per_lane: 2/4/8 rows in flight, 3/5/9 = pipelined 2/4/8 (default: pipelined 4)
-    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 5u;
+    // 64 blocks per CU: far more tiles in flight than are resident, so waves that
+    // draw short tiles are replaced at once (measured, profiles/r01_sweep_*.jsonl)
+    const dim3 grid(grid_for(4, tiles, 64));
+    // loads_per_lane: 2/4/8 rows in flight, 3/5/9 = pipelined 2/4/8 (default: 4)
+    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 4u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {

@@ -54,8 +54,8 @@ def main():
             arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
             run = lambda: engine.checksum_ragged(arena, desc, pseudo)  # noqa: E731
-            shapes = [(0, u, b, True) for u in (2, 4, 8, 3, 5, 9) for b in (0, 4096, 8192, 16384)]
-            shapes += [(0, 5, 0, False)]
+            shapes = [(0, u, b, True) for u in (2, 4, 3, 5) for b in (0, 8192, 32768, 65536)]
+            shapes += [(0, 4, 0, False)]
         else:
             arena = torch.empty(n * w.stride, dtype=torch.uint8, device="cuda")
             engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
