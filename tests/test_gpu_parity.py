@@ -195,7 +195,7 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt):
              (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
     try:
         for stride, length in cases:
-            for blocks in (0, 1, 7):
+            for blocks in (0, 1, 7, 9, 17):  # < 8 blocks: one group; 9/17: uneven XCD groups
                 engine.tune(0, rows, blocks, plain_loads=not nt)
                 n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
                 host = rng.integers(0, 256, n * stride, dtype=np.uint8)
@@ -275,6 +275,27 @@ def test_ragged_vs_oracle(oracle, n):
         got = u16(engine.checksum_ragged(arena, desc, pseudo))
         want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
         assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
+
+
+@pytest.mark.parametrize("blocks", [1, 3, 8, 9, 17])
+@pytest.mark.parametrize("xcd", [True, False])
+@pytest.mark.parametrize("rows", [2, 4, 8, 3, 5, 9])
+def test_ragged_launch_shapes(oracle, blocks, xcd, rows):
+    """Every ragged row depth (plain and pipelined), grids smaller and larger
+    than the 8 XCD groups, tiles left over after the groups split."""
+    rng = np.random.default_rng(blocks * 100 + rows * 2 + xcd)
+    n = 64 * 23 + 5
+    offs, lens, size = _ragged_case(rng, n, 3000)
+    host = rng.integers(0, 256, size + 16, dtype=np.uint8)
+    _, arena = upload(host, 0)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, 7, 6)
+    desc = engine.make_desc(offs, lens, np.arange(n) % N_FLOWS)
+    engine.tune(0, rows, blocks, xcd_groups=xcd)
+    try:
+        got = u16(engine.checksum_ragged(arena, desc, pseudo))
+    finally:
+        engine.tune()
+    assert np.array_equal(got, oracle.batch_ragged(host, offs, lens, 4, 6, 7, N_FLOWS, 0))
 
 
 def test_ragged_out_of_domain_flags_error(oracle):

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Kernel throughput vs batch size, with and without the XCD-grouped task split.
+
+    python tools/size_scan.py [--iters 10]
+
+One JSON line per (workload, packets, xcd_groups): median kernel ms (HIP
+events) and algorithmic GB/s.  Both arms run in one process, interleaved.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from pip_amd import engine  # noqa: E402
+from pip_amd.workloads import CFG4, CFG5, N_FLOWS  # noqa: E402
+
+
+def timed(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return statistics.median(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    engine.require_gpu()
+    for w, sizes in ((CFG5, (2 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))):
+        pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
+        for n in sizes:
+            if w.ragged:
+                arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
+                nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
+                run = lambda: engine.checksum_ragged(arena, desc, pseudo)  # noqa: E731
+            else:
+                arena = torch.empty(n * w.stride, dtype=torch.uint8, device="cuda")
+                engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
+                nbytes = (w.length + 2) * n
+                run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
+            res = {}
+            for rnd in range(3):
+                for xcd in (True, False):
+                    engine.tune(xcd_groups=xcd)
+                    res.setdefault(xcd, []).append(timed(run, a.iters))
+                    out = run()
+                    if xcd:
+                        ref = out.clone()
+                    else:
+                        assert torch.equal(out, ref)
+            for xcd, ms in res.items():
+                m = statistics.median(ms)
+                print(json.dumps({"workload": w.name, "packets": n, "gbytes": round(nbytes / 1e9, 1),
+                                  "xcd_groups": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}),
+                      flush=True)
+            engine.tune()
+            del arena
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
