@@ -141,6 +141,57 @@ __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
     return {b + (uint64_t)gi * 4 + w, e, (uint64_t)nb * 4};
 }
 
+// Task cursor of one wave.  Static: grid-stride over the (XCD group's) task
+// range.  Dynamic (queue != nullptr): waves claim the next task of their group
+// from a device counter, one atomic per task issued a task ahead, so the tasks
+// in flight on the whole chip stay a contiguous window sliding through the
+// arena (zeroed by the launcher before every launch).
+constexpr uint32_t kQueueStride = 16;  // counters 64 B apart
+struct TaskCursor {
+    uint64_t cur, end, step, base;
+    unsigned long long* q;
+    unsigned long long pending;  // lane 0: the claim for the task after `cur`, still in flight
+
+    __device__ __forceinline__ unsigned long long issue_claim() const {
+        unsigned long long v = 0;
+        if ((threadIdx.x & 63) == 0) v = atomicAdd(q, 1ull);
+        return v;
+    }
+    __device__ __forceinline__ uint64_t take(unsigned long long v) const {
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        return base + (((uint64_t)hi << 32) | lo);
+    }
+    __device__ __forceinline__ void init(uint64_t n_tasks, uint32_t kflags, unsigned long long* queue) {
+        const bool grouped = (kflags & kNoXcdGroups) == 0 && gridDim.x >= 8;
+        const uint32_t g = grouped ? (blockIdx.x & 7) : 0;
+        q = queue;
+        pending = 0;
+        if (queue) {
+            base = grouped ? n_tasks * g / 8 : 0;
+            end = grouped ? n_tasks * (g + 1) / 8 : n_tasks;
+            q = queue + g * kQueueStride;
+            step = 0;
+            cur = take(issue_claim());
+            if (cur < end) pending = issue_claim();
+        } else {
+            const TaskRange r = xcd_tasks(n_tasks, grouped);
+            cur = r.first;
+            end = r.end;
+            step = r.step;
+        }
+    }
+    __device__ __forceinline__ bool ok() const { return cur < end; }
+    __device__ __forceinline__ void advance() {
+        if (q) {
+            cur = take(pending);  // the claim issued one task ago has landed by now
+            if (cur < end) pending = issue_claim();
+        } else {
+            cur += step;
+        }
+    }
+};
+
 __device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -227,15 +278,18 @@ template <int U, bool PIPE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
                                               uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                                              unsigned long long* __restrict__ queue) {
     const int lane = threadIdx.x & 63;
     const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     const uint32_t lterm = len_term(len);
     const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
     const uint64_t n_tasks = (n + run - 1) / run;
-    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kNoXcdGroups) == 0);
-    for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
+    TaskCursor tc;
+    tc.init(n_tasks, kflags, queue);
+    for (; tc.ok(); tc.advance()) {
+        const uint64_t task = tc.cur;
         const uint64_t p0 = task * run;
         const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
         const uint32_t tchunks = np * cpp;
@@ -486,7 +540,21 @@ static const Variant& pick_variant(uint32_t nch) {
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t, unsigned long long*);
+
+// Per-device task counters of the dynamic work queue (8 XCD groups, 64 B apart).
+static std::mutex g_queue_mu;
+static std::vector<unsigned long long*> g_queue_dev(64, nullptr);
+static int task_queue(unsigned long long** out) {
+    int dev = 0;
+    PIPCK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(g_queue_mu);
+    if ((size_t)dev >= g_queue_dev.size()) g_queue_dev.resize(dev + 1, nullptr);
+    if (!g_queue_dev[dev]) PIPCK_HIP(hipMalloc(&g_queue_dev[dev], 8 * kQueueStride * sizeof(unsigned long long)));
+    *out = g_queue_dev[dev];
+    return PIPCK_OK;
+}
+constexpr uint32_t kDynamicQueue = 16u;  // pipck_tune flags bit 4
 struct FlatVariant {
     int u;
     bool pipe;
@@ -568,10 +636,18 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t rows = (g_tune.flags.load() >> 8) ? (g_tune.flags.load() >> 8) : 128u;
         const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
-        const uint32_t grid = grid_for(4, tasks, 64);
+        const uint32_t flags = g_tune.flags.load();
+        unsigned long long* queue = nullptr;
+        uint32_t grid = grid_for(4, tasks, 64);
+        if (flags & kDynamicQueue) {  // claimed tasks: one resident-sized grid is enough
+            int rc = task_queue(&queue);
+            if (rc) return rc;
+            PIPCK_HIP(hipMemsetAsync(queue, 0, 8 * kQueueStride * sizeof(unsigned long long), as_stream(stream)));
+            if (!g_tune.blocks.load()) grid = grid_for(4, tasks, 4);
+        }
         hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), 0, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
-                           flow_origin, d_out, d_ok, g_tune.flags.load());
+                           flow_origin, d_out, d_ok, flags, queue);
         PIPCK_LAUNCHED("k_flat");
         return PIPCK_OK;
     }

@@ -54,19 +54,23 @@ def main():
                 nbytes = (w.length + 2) * n
                 run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             res = {}
+            arms = {"static": {}, "queue": {"dynamic_queue": True}, "queue_1024": {"dynamic_queue": True, "blocks": 1024},
+                    "queue_4096": {"dynamic_queue": True, "blocks": 4096}}
+            if w.ragged:
+                arms = {"static": {}, "no_xcd": {"xcd_groups": False}}
             for rnd in range(3):
-                for xcd in (True, False):
-                    engine.tune(xcd_groups=xcd)
+                for xcd, kw in arms.items():
+                    engine.tune(**kw)
                     res.setdefault(xcd, []).append(timed(run, a.iters))
                     out = run()
-                    if xcd:
+                    if xcd == "static":
                         ref = out.clone()
                     else:
                         assert torch.equal(out, ref)
             for xcd, ms in res.items():
                 m = statistics.median(ms)
                 print(json.dumps({"workload": w.name, "packets": n, "gbytes": round(nbytes / 1e9, 1),
-                                  "xcd_groups": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}),
+                                  "arm": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}),
                       flush=True)
             engine.tune()
             del arena
