@@ -39,4 +39,18 @@ uint16_t pip_inet_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, stru
 uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
                                 struct in6_addr dst);
 
+// ---- deferred forms for a batched TX path ----
+// Queue a packet on this thread's TX queue instead of checksumming it now; the
+// chain's bytes are copied at call time.  pip_checksum_amd_flush() checksums
+// every queued packet on the GPU in one batch and stores htons(checksum) into
+// each csum_field (what pip_tcp_packet.cpp:132-133 / pip_udp.cpp:51,61 /
+// pip_netif.cpp:97 store), so it must run before those packets are output.
+void pip_inet_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src,
+                                    struct in_addr dst, void* csum_field);
+void pip_inet6_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
+                                     struct in6_addr dst, void* csum_field);
+void pip_ip_checksum_deferred(const void* hdr, uint32_t len, void* csum_field);
+uint64_t pip_checksum_amd_pending();
+void pip_checksum_amd_flush();
+
 #endif

@@ -175,6 +175,31 @@ int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stri
 void* pipck_host_alloc(size_t bytes);   /* pinned host memory */
 void  pipck_host_free(void* p);
 
+/* ---- deferred TX queue -------------------------
+ * pip checksums each segment synchronously while building it
+ * (pip/protocol/pip_tcp_packet.cpp:124-134, pip/protocol/pip_udp.cpp:50-51,
+ * 60-61, pip/pip_netif.cpp:97).  A TX queue defers that: packets are added with
+ * their bytes (the payloads of a pip_buf chain, in order), their pseudo-header
+ * and the address of their 16-bit checksum field; pipck_txq_flush copies the
+ * batch to the device, checksums all of it in one pass and stores
+ * htons(result) into every field -- exactly the bytes pip would have written.
+ * Bytes are copied at add time, so buffers may be reused after add; the
+ * checksum fields must stay valid until flush.  One queue per thread. */
+typedef struct pipck_txq pipck_txq;
+int pipck_txq_create(pipck_ctx* ctx, pipck_txq** out);
+int pipck_txq_destroy(pipck_txq* q);
+/* pip_inet_checksum_buf (pip_checksum.cpp:90-115): src/dst as in_addr.s_addr */
+int pipck_txq_add4(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, uint32_t src, uint32_t dst,
+                   void* csum_field);
+/* pip_inet6_checksum_buf (pip_checksum.cpp:118-148): src/dst as in6_addr bytes */
+int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
+                   const uint8_t* dst, void* csum_field);
+/* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
+int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);
+uint64_t pipck_txq_pending(const pipck_txq* q);
+/* Synchronous: returns once every queued field holds its checksum; the queue is then empty. */
+int pipck_txq_flush(pipck_txq* q);
+
 #ifdef __cplusplus
 }
 #endif

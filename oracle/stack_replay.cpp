@@ -149,6 +149,81 @@ static void tcp_session(const Peer& pe, uint16_t mss, uint32_t write_len) {
     g_tcp->close();
 }
 
+#ifdef PIPCK_DEFERRED_CHECK
+#include "pip_checksum_amd.h"
+
+// The deferred (batched) TX API of libpip_checksum_amd.so on real pip_buf
+// chains built by pip's own pip_buf class: every emitted IPv4 header and
+// TCP/UDP segment is rebuilt as a chain (header with its checksum zeroed ->
+// payload split at an odd offset), queued, and flushed in one batch; each
+// stored field must equal the checksum pip put on the wire.  Printed to
+// stderr so stdout stays comparable with pip's own build.
+static void deferred_check() {
+    struct Item {
+        std::vector<uint8_t> hdr, body;
+        uint8_t field[2];
+        uint16_t wire;
+    };
+    std::vector<Item> items(g_out.size() * 2);
+    std::vector<std::shared_ptr<pip_buf>> keep;
+    size_t k = 0;
+    for (auto& pk : g_out) {
+        const int ver = pk[0] >> 4;
+        const size_t hl = ver == 4 ? 20 : 40;
+        const uint8_t proto = ver == 4 ? pk[9] : pk[6];
+        const size_t csum_off = proto == IPPROTO_TCP ? 16 : 6;
+        const size_t l4h = proto == IPPROTO_TCP ? (pk[hl + 12] >> 4) * 4 : 8;
+        if (ver == 4) {  // pip_ip_checksum of the IPv4 header
+            Item& it = items[k++];
+            it.hdr.assign(pk.begin(), pk.begin() + 20);
+            it.wire = (uint16_t)(it.hdr[10] << 8 | it.hdr[11]);
+            it.hdr[10] = it.hdr[11] = 0;
+            pip_ip_checksum_deferred(it.hdr.data(), 20, it.field);
+        }
+        Item& it = items[k++];
+        it.hdr.assign(pk.begin() + hl, pk.begin() + hl + l4h);
+        it.body.assign(pk.begin() + hl + l4h, pk.end());
+        it.wire = (uint16_t)(it.hdr[csum_off] << 8 | it.hdr[csum_off + 1]);
+        it.hdr[csum_off] = it.hdr[csum_off + 1] = 0;
+        auto head = std::make_shared<pip_buf>(it.hdr.data(), (pip_uint32)it.hdr.size(), 0);
+        if (!it.body.empty()) {
+            const size_t cut = it.body.size() > 1 ? (it.body.size() / 2) | 1 : it.body.size();  // odd split
+            auto b1 = std::make_shared<pip_buf>(it.body.data(), (pip_uint32)cut, 0);
+            head->set_next(b1);
+            if (cut < it.body.size()) {
+                auto b2 = std::make_shared<pip_buf>(it.body.data() + cut, (pip_uint32)(it.body.size() - cut), 0);
+                b1->set_next(b2);
+                keep.push_back(b2);
+            }
+            keep.push_back(b1);
+        }
+        keep.push_back(head);
+        // an odd middle segment restarts pip's byte pairing, so compare against pip's
+        // synchronous answer on the same chain, and that against the wire when the split is even
+        struct in6_addr s6, d6;
+        if (ver == 4) {
+            struct in_addr s, d;
+            memcpy(&s, &pk[12], 4);
+            memcpy(&d, &pk[16], 4);
+            it.wire = pip_inet_checksum_buf(head, proto, s, d);
+            pip_inet_checksum_buf_deferred(head, proto, s, d, it.field);
+        } else {
+            memcpy(&s6, &pk[8], 16);
+            memcpy(&d6, &pk[24], 16);
+            it.wire = pip_inet6_checksum_buf(head, proto, s6, d6);
+            pip_inet6_checksum_buf_deferred(head, proto, s6, d6, it.field);
+        }
+    }
+    const unsigned long long pending = pip_checksum_amd_pending();
+    pip_checksum_amd_flush();
+    int bad = 0;
+    for (size_t i = 0; i < k; i++)
+        if ((uint16_t)(items[i].field[0] << 8 | items[i].field[1]) != items[i].wire) bad++;
+    fprintf(stderr, "DEFERRED queued %llu checked %zu bad %d pending_after %llu\n", pending, k, bad,
+            (unsigned long long)pip_checksum_amd_pending());
+}
+#endif
+
 int main() {
     // Touch the checksum provider once so any one-time initialisation happens
     // before pip's 1 s retransmit clock starts on the first queued segment.
@@ -185,6 +260,9 @@ int main() {
         printf("\n");
     }
     printf("PACKETS %zu VERIFY_BAD %d\n", g_out.size(), bad);
+#ifdef PIPCK_DEFERRED_CHECK
+    deferred_check();
+#endif
     fflush(stdout);
     _exit(0);  // pip's timer thread is detached and never stops
 }

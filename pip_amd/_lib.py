@@ -62,6 +62,13 @@ SIGNATURES = {
     "pipck_host_checksum_fixed": (_i32, [_p, _p, _u64, _u32, _u64, _i32, _p, _u32, _u64, _p]),
     "pipck_host_alloc": (_p, [_sz]),
     "pipck_host_free": (None, [_p]),
+    "pipck_txq_create": (_i32, [_p, C.POINTER(_p)]),
+    "pipck_txq_destroy": (_i32, [_p]),
+    "pipck_txq_add4": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _u32, _u32, _p]),
+    "pipck_txq_add6": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _p, _p, _p]),
+    "pipck_txq_add_ip": (_i32, [_p, _p, _u32, _p]),
+    "pipck_txq_pending": (_u64, [_p]),
+    "pipck_txq_flush": (_i32, [_p]),
 }
 
 _lib = None

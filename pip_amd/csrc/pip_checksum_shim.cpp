@@ -25,7 +25,9 @@ namespace {
 
 struct ThreadCtx {
     pipck_ctx* ctx = nullptr;
+    pipck_txq* txq = nullptr;
     ~ThreadCtx() {
+        if (txq) pipck_txq_destroy(txq);
         if (ctx) pipck_ctx_destroy(ctx);
     }
     pipck_ctx* get() {
@@ -34,6 +36,13 @@ struct ThreadCtx {
             if (rc) die("pipck_ctx_create", rc);
         }
         return ctx;
+    }
+    pipck_txq* queue() {
+        if (!txq) {
+            int rc = pipck_txq_create(get(), &txq);
+            if (rc) die("pipck_txq_create", rc);
+        }
+        return txq;
     }
 };
 thread_local ThreadCtx t_ctx;
@@ -58,27 +67,38 @@ uint32_t v6_terms(const in6_addr& a) {
     return s;
 }
 
-// Collect a chain's segments in order (pip_checksum.cpp:145).
-uint16_t chain_checksum(const std::shared_ptr<pip_buf>& buf, uint32_t pseudo) {
-    const pip_buf_layout* head = reinterpret_cast<const pip_buf_layout*>(buf.get());
+// A chain's segments in order (pip_checksum.cpp:145), read through the layout view.
+struct ChainSegs {
     pipck_hseg local[8];
     pipck_hseg* segs = local;
     uint32_t n = 0, cap = 8;
-    for (const pip_buf_layout* q = head; q; q = q->next) {
-        if (n == cap) {
-            pipck_hseg* bigger = (pipck_hseg*)std::malloc(sizeof(pipck_hseg) * cap * 2);
-            if (!bigger) die("malloc", PIPCK_ENOMEM);
-            std::memcpy(bigger, segs, sizeof(pipck_hseg) * n);
-            if (segs != local) std::free(segs);
-            segs = bigger;
-            cap *= 2;
+    uint32_t total_len = 0;
+    explicit ChainSegs(const std::shared_ptr<pip_buf>& buf) {
+        const pip_buf_layout* head = reinterpret_cast<const pip_buf_layout*>(buf.get());
+        total_len = head->total_len;
+        for (const pip_buf_layout* q = head; q; q = q->next) {
+            if (n == cap) {
+                pipck_hseg* bigger = (pipck_hseg*)std::malloc(sizeof(pipck_hseg) * cap * 2);
+                if (!bigger) die("malloc", PIPCK_ENOMEM);
+                std::memcpy(bigger, segs, sizeof(pipck_hseg) * n);
+                if (segs != local) std::free(segs);
+                segs = bigger;
+                cap *= 2;
+            }
+            segs[n++] = pipck_hseg{q->payload, q->payload_len};
         }
-        segs[n++] = pipck_hseg{q->payload, q->payload_len};
     }
+    ~ChainSegs() {
+        if (segs != local) std::free(segs);
+    }
+    ChainSegs(const ChainSegs&) = delete;
+    ChainSegs& operator=(const ChainSegs&) = delete;
+};
+
+uint16_t chain_checksum(const std::shared_ptr<pip_buf>& buf, uint32_t pseudo) {
+    ChainSegs c(buf);
     // length term: the head's u32 total_len split hi + lo (pip_checksum.cpp:140-142)
-    const uint32_t total = head->total_len;
-    const uint32_t sum = device_sum(segs, n, pseudo + split(total));
-    if (segs != local) std::free(segs);
+    const uint32_t sum = device_sum(c.segs, c.n, pseudo + split(c.total_len));
     return (uint16_t)~(uint16_t)sum;
 }
 
@@ -114,4 +134,34 @@ uint16_t pip_inet_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, stru
 uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
                                 struct in6_addr dst) {
     return chain_checksum(buf, v6_terms(src) + v6_terms(dst) + proto);
+}
+
+// ---- deferred forms (batched TX path) -------------------------------------
+// The queue computes the pseudo-header from the addresses itself and takes the
+// length term from the queued bytes, which for a pip_buf chain equals the
+// head's total_len (pip/pip_buf.h:81-97 keeps it as the sum of the segments).
+void pip_inet_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src,
+                                    struct in_addr dst, void* csum_field) {
+    ChainSegs c(buf);
+    int rc = pipck_txq_add4(t_ctx.queue(), c.segs, c.n, proto, src.s_addr, dst.s_addr, csum_field);
+    if (rc) die("pipck_txq_add4", rc);
+}
+
+void pip_inet6_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
+                                     struct in6_addr dst, void* csum_field) {
+    ChainSegs c(buf);
+    int rc = pipck_txq_add6(t_ctx.queue(), c.segs, c.n, proto, src.s6_addr, dst.s6_addr, csum_field);
+    if (rc) die("pipck_txq_add6", rc);
+}
+
+void pip_ip_checksum_deferred(const void* hdr, uint32_t len, void* csum_field) {
+    int rc = pipck_txq_add_ip(t_ctx.queue(), hdr, len, csum_field);
+    if (rc) die("pipck_txq_add_ip", rc);
+}
+
+uint64_t pip_checksum_amd_pending() { return pipck_txq_pending(t_ctx.queue()); }
+
+void pip_checksum_amd_flush() {
+    int rc = pipck_txq_flush(t_ctx.queue());
+    if (rc) die("pipck_txq_flush", rc);
 }

@@ -35,3 +35,9 @@ def test_pip_stack_on_amd_checksum_is_byte_identical():
     assert got[-1] == want[-1]
     diff = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert not diff and len(got) == len(want), diff[:5]
+    # the deferred (batched) API on real pip_buf chains, flushed in one GPU batch
+    line = [ln for ln in r.stderr.splitlines() if ln.startswith("DEFERRED")]
+    assert line, r.stderr[-2000:]
+    f = line[-1].split()
+    assert f[f.index("bad") + 1] == "0" and f[f.index("pending_after") + 1] == "0", line
+    assert int(f[f.index("checked") + 1]) >= 40

@@ -477,3 +477,55 @@ def test_full_size_ragged(oracle):
     assert int((again != 0).sum().item()) == 0
     del arena, desc, out, again
     torch.cuda.empty_cache()
+
+
+# ----------------------------------------------------------------------------
+# 9. deferred TX queue: mixed v4/v6 chains + IPv4 headers
+# ----------------------------------------------------------------------------
+def test_txq_mixed_batches_vs_oracle(oracle):
+    lib = _lib.load()
+    ctx, q = C.c_void_p(), C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    rng = np.random.default_rng(99)
+    try:
+        for n_pk in (1, 300, 5000):  # the queue is reused and grows
+            fields = (C.c_uint8 * (2 * n_pk))()
+            keep, want = [], []
+            for i in range(n_pk):
+                kind = int(rng.integers(0, 3))
+                field = C.c_void_p(C.addressof(fields) + 2 * i)
+                if kind == 2:  # IPv4 header, ip_sum = 0
+                    hdr = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+                    hdr[10:12] = b"\0\0"
+                    buf = C.create_string_buffer(bytes(hdr), 20)
+                    keep.append(buf)
+                    _lib.check("add_ip", lib.pipck_txq_add_ip(q, buf, 20, field))
+                    want.append(oracle.ip_checksum(bytes(hdr)))
+                    continue
+                segs = [rng.integers(0, 256, int(rng.choice([20, 8, rng.integers(0, 9), rng.integers(0, 9000)])),
+                                     dtype=np.uint8).tobytes() for _ in range(int(rng.integers(1, 4)))]
+                arr = (_lib.HSeg * len(segs))()
+                for j, sgm in enumerate(segs):
+                    b = C.create_string_buffer(sgm, max(len(sgm), 1))
+                    keep.append(b)
+                    arr[j].ptr = C.cast(b, C.c_void_p)
+                    arr[j].len = len(sgm)
+                proto = int(rng.choice([6, 17]))
+                if kind == 0:
+                    s, d = rng.bytes(4), rng.bytes(4)
+                    _lib.check("add4", lib.pipck_txq_add4(q, arr, len(segs), proto, int.from_bytes(s, "little"),
+                                                          int.from_bytes(d, "little"), field))
+                    want.append(oracle.inet_checksum_chain(segs, proto, s, d))
+                else:
+                    s, d = rng.bytes(16), rng.bytes(16)
+                    _lib.check("add6", lib.pipck_txq_add6(q, arr, len(segs), proto, s, d, field))
+                    want.append(oracle.inet6_checksum_chain(segs, proto, s, d))
+            assert lib.pipck_txq_pending(q) == n_pk
+            _lib.check("pipck_txq_flush", lib.pipck_txq_flush(q))
+            assert lib.pipck_txq_pending(q) == 0
+            got = np.frombuffer(bytes(fields), dtype=">u2")  # htons(result), as pip stores it
+            assert np.array_equal(got, np.array(want, dtype=np.uint16)), n_pk
+    finally:
+        lib.pipck_txq_destroy(q)
+        lib.pipck_ctx_destroy(ctx)
