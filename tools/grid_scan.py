@@ -28,7 +28,7 @@ def main():
     engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
     run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
     ref = run().clone()
-    arms = list(itertools.product((1024, 2048, 4096, 16384, 65536), (64, 128, 512, 2048)))
+    arms = list(itertools.product((16384, 65536, 131072, 1 << 30), (32, 64, 128, 256)))
     res = {}
     for _ in range(3):
         for blocks, rows in arms:
