@@ -114,24 +114,19 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
 }
 
 // ---------------------------------------------------------------------------
-// flat-stream kernel: fixed strides of whole 16-byte chunks, >= 64 chunks each
+// task split shared by the streaming kernels
 // ---------------------------------------------------------------------------
-// A wave owns a run of consecutive packets and streams their chunks as
-// consecutive 1 KiB rows (lane l of row r reads chunk 64r + l): every load
-// instruction is one fully coalesced 1 KiB read, U rows are in flight per
-// wave, and since a packet spans >= 64 chunks a row holds at most one packet
-// boundary.  Lanes keep a running u64 sum for the packet the row is in; at a
-// boundary the finished packet's partials are folded and wave-reduced once.
-// XCD-grouped work split.  The dispatcher deals blocks round-robin over the 8
-// XCDs, so blocks with equal blockIdx % 8 share an XCD -- its L2 and its
-// address-translation caches.  Each such group takes one contiguous eighth of
-// the tasks, so an XCD streams one region of the arena instead of all of them
-// (arenas of 75-150 GB otherwise lose 5-10 % to translation misses).  Speed
-// only: any placement computes the same results.
+// Static grid-stride over tasks; with the default grid (one task per wave,
+// grid_for(.., 0)) the in-order block dispatcher then acts as the task queue.
+// XCD grouping (default on, pipck_tune flags bit 3 turns it off): the
+// dispatcher deals blocks round-robin over the 8 XCDs, so blocks with equal
+// blockIdx % 8 share an XCD -- its L2 and address-translation caches -- and
+// each such group takes one contiguous eighth of the tasks.  Speed only: any
+// placement computes the same results.
 struct TaskRange {
     uint64_t first, end, step;
 };
-constexpr uint32_t kNoXcdGroups = 8u;  // pipck_tune flags bit 3
+constexpr uint32_t kNoXcdGroups = 8u;
 __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
     const uint32_t w = threadIdx.x >> 6;
     if (!grouped || gridDim.x < 8) return {(uint64_t)blockIdx.x * 4 + w, n_tasks, (uint64_t)gridDim.x * 4};
@@ -141,57 +136,15 @@ __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
     return {b + (uint64_t)gi * 4 + w, e, (uint64_t)nb * 4};
 }
 
-// Task cursor of one wave.  Static: grid-stride over the (XCD group's) task
-// range.  Dynamic (queue != nullptr): waves claim the next task of their group
-// from a device counter, one atomic per task issued a task ahead, so the tasks
-// in flight on the whole chip stay a contiguous window sliding through the
-// arena (zeroed by the launcher before every launch).
-constexpr uint32_t kQueueStride = 16;  // counters 64 B apart
-struct TaskCursor {
-    uint64_t cur, end, step, base;
-    unsigned long long* q;
-    unsigned long long pending;  // lane 0: the claim for the task after `cur`, still in flight
-
-    __device__ __forceinline__ unsigned long long issue_claim() const {
-        unsigned long long v = 0;
-        if ((threadIdx.x & 63) == 0) v = atomicAdd(q, 1ull);
-        return v;
-    }
-    __device__ __forceinline__ uint64_t take(unsigned long long v) const {
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-        return base + (((uint64_t)hi << 32) | lo);
-    }
-    __device__ __forceinline__ void init(uint64_t n_tasks, uint32_t kflags, unsigned long long* queue) {
-        const bool grouped = (kflags & kNoXcdGroups) == 0 && gridDim.x >= 8;
-        const uint32_t g = grouped ? (blockIdx.x & 7) : 0;
-        q = queue;
-        pending = 0;
-        if (queue) {
-            base = grouped ? n_tasks * g / 8 : 0;
-            end = grouped ? n_tasks * (g + 1) / 8 : n_tasks;
-            q = queue + g * kQueueStride;
-            step = 0;
-            cur = take(issue_claim());
-            if (cur < end) pending = issue_claim();
-        } else {
-            const TaskRange r = xcd_tasks(n_tasks, grouped);
-            cur = r.first;
-            end = r.end;
-            step = r.step;
-        }
-    }
-    __device__ __forceinline__ bool ok() const { return cur < end; }
-    __device__ __forceinline__ void advance() {
-        if (q) {
-            cur = take(pending);  // the claim issued one task ago has landed by now
-            if (cur < end) pending = issue_claim();
-        } else {
-            cur += step;
-        }
-    }
-};
-
+// ---------------------------------------------------------------------------
+// flat-stream kernel: fixed strides of whole 16-byte chunks, >= 64 chunks each
+// ---------------------------------------------------------------------------
+// A wave owns a run of consecutive packets and streams their chunks as
+// consecutive 1 KiB rows (lane l of row r reads chunk 64r + l): every load
+// instruction is one fully coalesced 1 KiB read, U rows are in flight per
+// wave, and since a packet spans >= 64 chunks a row holds at most one packet
+// boundary.  Lanes keep a running u64 sum for the packet the row is in; at a
+// boundary the finished packet's partials are folded and wave-reduced once.
 __device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -278,18 +231,15 @@ template <int U, bool PIPE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
                                               uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
-                                              unsigned long long* __restrict__ queue) {
+                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
     const int lane = threadIdx.x & 63;
     const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     const uint32_t lterm = len_term(len);
     const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
     const uint64_t n_tasks = (n + run - 1) / run;
-    TaskCursor tc;
-    tc.init(n_tasks, kflags, queue);
-    for (; tc.ok(); tc.advance()) {
-        const uint64_t task = tc.cur;
+    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kNoXcdGroups) == 0);
+    for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
         const uint64_t p0 = task * run;
         const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
         const uint32_t tchunks = np * cpp;
@@ -540,21 +490,7 @@ static const Variant& pick_variant(uint32_t nch) {
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t, unsigned long long*);
-
-// Per-device task counters of the dynamic work queue (8 XCD groups, 64 B apart).
-static std::mutex g_queue_mu;
-static std::vector<unsigned long long*> g_queue_dev(64, nullptr);
-static int task_queue(unsigned long long** out) {
-    int dev = 0;
-    PIPCK_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(g_queue_mu);
-    if ((size_t)dev >= g_queue_dev.size()) g_queue_dev.resize(dev + 1, nullptr);
-    if (!g_queue_dev[dev]) PIPCK_HIP(hipMalloc(&g_queue_dev[dev], 8 * kQueueStride * sizeof(unsigned long long)));
-    *out = g_queue_dev[dev];
-    return PIPCK_OK;
-}
-constexpr uint32_t kDynamicQueue = 16u;  // pipck_tune flags bit 4
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
 struct FlatVariant {
     int u;
     bool pipe;
@@ -584,12 +520,16 @@ static const FlatVariant& flat_variant(uint32_t loads) {
     }
 }
 
-// Default grid: blocks_per_cu 256-thread blocks per CU (more than are resident
-// at once: blocks that finish early are replaced, which balances the tail).
+// Default grid: blocks_per_cu 256-thread blocks per CU, or (0) one block per
+// 4 work units -- every wave then takes exactly one task, and the in-order
+// block dispatcher works as the task queue: the tasks in flight on the chip are
+// always a contiguous window sliding through the arena (measured best; an
+// explicit atomic queue or a resident-sized grid-stride grid lost 3-15 %,
+// profiles/r01_grid_scan*.jsonl).
 static uint32_t grid_for(uint64_t units_per_block_iter, uint64_t n, uint32_t blocks_per_cu = 8) {
     uint64_t need = (n + units_per_block_iter - 1) / units_per_block_iter;
     uint64_t cap = g_tune.blocks.load();
-    if (!cap) cap = (uint64_t)device_cus() * blocks_per_cu;
+    if (!cap) cap = blocks_per_cu ? (uint64_t)device_cus() * blocks_per_cu : 0x7FFFFFFFull;
     if (need > cap) need = cap;
     return (uint32_t)(need ? need : 1);
 }
@@ -631,23 +571,16 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // rows in flight per wave: 16 for jumbo packets, 8 below 4 KiB (measured, profiles/README.md)
         const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (cpp >= 256 ? 16u : 8u);
         const FlatVariant* fv = &flat_variant(loads);
-        // a wave task covers ~128 rows of 1 KiB (measured best for 1.5-9 KiB packets):
-        // the row pipeline rarely restarts and consecutive waves stream adjacent 128 KiB spans
-        const uint32_t rows = (g_tune.flags.load() >> 8) ? (g_tune.flags.load() >> 8) : 128u;
+        // a wave task covers ~32 rows of 1 KiB and the grid holds one task per wave
+        // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_grid_scan*.jsonl)
+        const uint32_t flags = g_tune.flags.load();
+        const uint32_t rows = (flags >> 8) ? (flags >> 8) : 32u;
         const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
-        const uint32_t flags = g_tune.flags.load();
-        unsigned long long* queue = nullptr;
-        uint32_t grid = grid_for(4, tasks, 64);
-        if (flags & kDynamicQueue) {  // claimed tasks: one resident-sized grid is enough
-            int rc = task_queue(&queue);
-            if (rc) return rc;
-            PIPCK_HIP(hipMemsetAsync(queue, 0, 8 * kQueueStride * sizeof(unsigned long long), as_stream(stream)));
-            if (!g_tune.blocks.load()) grid = grid_for(4, tasks, 4);
-        }
+        const uint32_t grid = grid_for(4, tasks, 0);
         hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), 0, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
-                           flow_origin, d_out, d_ok, flags, queue);
+                           flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");
         return PIPCK_OK;
     }

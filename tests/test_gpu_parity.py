@@ -186,18 +186,18 @@ def test_fixed_every_shape_vs_oracle(oracle, lanes):
 
 @pytest.mark.parametrize("rows", [2, 4, 8, 16, 3, 5, 9])
 @pytest.mark.parametrize("nt", [False, True])
-@pytest.mark.parametrize("queue", [False, True])
-def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, queue):
+@pytest.mark.parametrize("xcd", [False, True])
+def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
     """The flat-stream fixed kernel (16-byte-multiple strides >= 1 KiB, aligned
     arena): packet boundaries at every lane position of a row, boundaries that
     fall exactly on row ends, stride padding wider than a row, runs cut short."""
-    rng = np.random.default_rng(rows * 10 + nt + 100 * queue)
+    rng = np.random.default_rng(rows * 10 + nt + 100 * xcd)
     cases = [(1024, 1024), (1024, 1023), (1024, 0), (1040, 1025), (1488, 1480), (1504, 1480), (2048, 17),
              (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
     try:
         for stride, length in cases:
             for blocks in (0, 1, 7, 9, 17):  # < 8 blocks: one group; 9/17: uneven XCD groups
-                engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, dynamic_queue=queue)
+                engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, xcd_groups=xcd)
                 n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
                 host = rng.integers(0, 256, n * stride, dtype=np.uint8)
                 if n > 2:

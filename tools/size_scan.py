@@ -54,10 +54,11 @@ def main():
                 nbytes = (w.length + 2) * n
                 run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             res = {}
-            arms = {"static": {}, "queue": {"dynamic_queue": True}, "queue_1024": {"dynamic_queue": True, "blocks": 1024},
-                    "queue_4096": {"dynamic_queue": True, "blocks": 4096}}
+            arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "grid_16384": {"blocks": 16384},
+                    "rows_128": {"rows_per_task": 128}}
             if w.ragged:
-                arms = {"static": {}, "no_xcd": {"xcd_groups": False}}
+                arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "grid_16384": {"blocks": 16384},
+                        "uncapped": {"blocks": 1 << 30}}
             for rnd in range(3):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
