@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     engine.require_gpu()
-    for w, sizes in ((CFG5, (2 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))):
+    for w, sizes in ((CFG5, (2 << 20, 4 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))):
         pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
         for n in sizes:
             if w.ragged:
@@ -54,12 +54,12 @@ def main():
                 nbytes = (w.length + 2) * n
                 run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             res = {}
-            arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "grid_16384": {"blocks": 16384},
-                    "rows_128": {"rows_per_task": 128}}
+            arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "rows_16": {"rows_per_task": 16},
+                    "no_xcd_rows_64": {"xcd_groups": False, "rows_per_task": 64}}
             if w.ragged:
-                arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "grid_16384": {"blocks": 16384},
-                        "uncapped": {"blocks": 1 << 30}}
-            for rnd in range(3):
+                arms = {"static": {}, "uncapped": {"blocks": 1 << 30},
+                        "uncapped_no_xcd": {"blocks": 1 << 30, "xcd_groups": False}}
+            for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
                     res.setdefault(xcd, []).append(timed(run, a.iters))
