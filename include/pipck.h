@@ -115,6 +115,10 @@ int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_
 int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
                        const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                        uint64_t flow_origin, uint8_t* d_ok, void* stream);
+/* The same for ragged batches (descriptors as for pipck_checksum_ragged);
+ * out-of-domain descriptors verify as 0 and set d_err. */
+int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
+                        const uint32_t* d_pseudo, uint8_t* d_ok, uint32_t* d_err, void* stream);
 
 /* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed

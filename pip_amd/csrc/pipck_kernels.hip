@@ -350,7 +350,8 @@ template <bool FINAL, int U, bool PIPE, bool NT>
 __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ arena, const pipck_desc* __restrict__ desc,
                                                 uint64_t n, const uint32_t* __restrict__ pseudo,
                                                 uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
-                                                uint32_t* __restrict__ err, uint32_t kflags) {
+                                                uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
+                                                uint32_t kflags) {
     __shared__ RaggedTileLds s_tile[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RaggedTileLds& t = s_tile[w];
@@ -404,7 +405,10 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
             const uint32_t F = bad ? 0u : be_fold(t.acc[lane], addr);
             if (FINAL) {
                 const uint32_t P = pseudo ? pseudo[d.flow] + len_term(len) : 0u;
-                out[seg] = bad ? (uint16_t)0 : finish(P, F);
+                if (ok)  // RX verification: valid iff the sum incl. the checksum field folds to 0xFFFF
+                    ok[seg] = !bad && fold16(P + F) == 0xFFFFu;
+                else
+                    out[seg] = bad ? (uint16_t)0 : finish(P, F);
             } else {
                 fseg[seg] = F;
             }
@@ -595,35 +599,36 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
 
 template <int U, bool PIPE>
 static void launch_ragged_u(bool final_, bool nt, dim3 grid, hipStream_t s, const uint8_t* a, const pipck_desc* d,
-                            uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint32_t* err) {
+                            uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint8_t* ok,
+                            uint32_t* err) {
     const uint32_t f = g_tune.flags.load();
     if (final_) {
-        if (nt) hipLaunchKernelGGL((k_ragged<true, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err, f);
-        else hipLaunchKernelGGL((k_ragged<true, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err, f);
+        if (nt) hipLaunchKernelGGL((k_ragged<true, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+        else hipLaunchKernelGGL((k_ragged<true, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
     } else {
-        if (nt) hipLaunchKernelGGL((k_ragged<false, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err, f);
-        else hipLaunchKernelGGL((k_ragged<false, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, err, f);
+        if (nt) hipLaunchKernelGGL((k_ragged<false, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+        else hipLaunchKernelGGL((k_ragged<false, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
     }
 }
 
 static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_desc, uint64_t n,
-                         const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint32_t* d_err,
+                         const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint8_t* d_ok, uint32_t* d_err,
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
-    // 64 blocks per CU: far more tiles in flight than are resident, so waves that
-    // draw short tiles are replaced at once (measured, profiles/r01_sweep_*.jsonl)
-    const dim3 grid(grid_for(4, tiles, 64));
+    // one tile per wave: the in-order dispatcher hands out tiles as waves finish
+    // (measured best, profiles/r01_size_scan*.jsonl)
+    const dim3 grid(grid_for(4, tiles, 0));
     // loads_per_lane: 2/4/8 rows in flight, 3/5/9 = pipelined 2/4/8 (default: 4)
     const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 4u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {
-        case 2: launch_ragged_u<2, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
-        case 4: launch_ragged_u<4, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
-        case 8: launch_ragged_u<8, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
-        case 3: launch_ragged_u<2, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
-        case 9: launch_ragged_u<8, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
-        default: launch_ragged_u<4, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_err); break;
+        case 2: launch_ragged_u<2, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 4: launch_ragged_u<4, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 8: launch_ragged_u<8, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 3: launch_ragged_u<2, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 9: launch_ragged_u<8, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        default: launch_ragged_u<4, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
     }
     PIPCK_LAUNCHED("k_ragged");
     return PIPCK_OK;
@@ -690,7 +695,17 @@ int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_
         set_error("pipck_checksum_ragged: null pointer");
         return PIPCK_EINVAL;
     }
-    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, d_out, nullptr, d_err, as_stream(stream));
+    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, d_out, nullptr, nullptr, d_err, as_stream(stream));
+}
+
+int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
+                        uint8_t* d_ok, uint32_t* d_err, void* stream) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_desc || !d_ok) {
+        set_error("pipck_verify_ragged: null pointer");
+        return PIPCK_EINVAL;
+    }
+    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, nullptr, nullptr, d_ok, d_err, as_stream(stream));
 }
 
 int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
@@ -703,7 +718,7 @@ int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_
     }
     hipStream_t s = as_stream(stream);
     if (n_segs) {
-        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, d_err, s);
+        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s);
         if (rc) return rc;
     }
     hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_segs, d_seg_begin,

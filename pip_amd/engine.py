@@ -102,6 +102,17 @@ def checksum_ragged(arena, desc, pseudo=None, out=None, err=None):
     return out
 
 
+def verify_ragged(arena, desc, pseudo=None, ok=None, err=None):
+    """RX verification of a ragged batch whose packets carry their checksum field."""
+    torch = _torch()
+    n = desc.shape[0]
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    call("pipck_verify_ragged", _ptr(arena), _ptr(desc), n, _ptr(pseudo), _ptr(ok), _ptr(err),
+         current_stream(arena.device))
+    return ok
+
+
 def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
     """segs: (n_segs, 2) int64 descriptors; seg_begin: (n_packets+1,) int64 CSR offsets."""
     torch = _torch()

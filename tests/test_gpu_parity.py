@@ -276,6 +276,8 @@ def test_ragged_vs_oracle(oracle, n):
         got = u16(engine.checksum_ragged(arena, desc, pseudo))
         want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
         assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
+        ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy().astype(bool)
+        assert np.array_equal(ok, got == 0)  # valid exactly when the recomputed checksum is 0x0000
 
 
 @pytest.mark.parametrize("blocks", [1, 3, 8, 9, 17])
@@ -475,6 +477,10 @@ def test_full_size_ragged(oracle):
     arena[o + 1] = (v & 0xFF).to(torch.uint8)
     again = engine.checksum_ragged(arena, desc, pseudo)
     assert int((again != 0).sum().item()) == 0
+    assert bool((engine.verify_ragged(arena, desc, pseudo) == 1).all())
+    arena[o[::5] + 2] ^= 0x41  # corrupt every fifth packet's destination port
+    ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy()
+    assert not ok[::5].any() and ok[np.arange(n) % 5 != 0].all()
     del arena, desc, out, again
     torch.cuda.empty_cache()
 
