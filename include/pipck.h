@@ -126,8 +126,8 @@ int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t 
  * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9 = pipelined
  * 2/4/8); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
  * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
- * fixed kernel, bit 3 = no XCD-grouped task split, bits 8.. = 1 KiB rows per
- * flat-kernel wave task (default 128). */
+ * fixed kernel, bit 3 = XCD-grouped task split, bits 8.. = 1 KiB rows per
+ * flat-kernel wave task (default 64). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */

@@ -117,16 +117,18 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
 // task split shared by the streaming kernels
 // ---------------------------------------------------------------------------
 // Static grid-stride over tasks; with the default grid (one task per wave,
-// grid_for(.., 0)) the in-order block dispatcher then acts as the task queue.
-// XCD grouping (default on, pipck_tune flags bit 3 turns it off): the
-// dispatcher deals blocks round-robin over the 8 XCDs, so blocks with equal
-// blockIdx % 8 share an XCD -- its L2 and address-translation caches -- and
-// each such group takes one contiguous eighth of the tasks.  Speed only: any
-// placement computes the same results.
+// grid_for(.., 0)) the in-order block dispatcher then acts as the task queue
+// and the tasks in flight form one contiguous window sliding through the arena.
+// Optional XCD grouping (pipck_tune flags bit 3): the dispatcher deals blocks
+// round-robin over the 8 XCDs, so blocks with equal blockIdx % 8 share an XCD
+// and each such group can take one contiguous eighth of the tasks (8 windows).
+// Measured: one window is as fast or faster from 38 to 151 GB
+// (profiles/r01_size_scan3.jsonl), so grouping is off by default.  Speed only:
+// any placement computes the same results.
 struct TaskRange {
     uint64_t first, end, step;
 };
-constexpr uint32_t kNoXcdGroups = 8u;
+constexpr uint32_t kXcdGroups = 8u;
 __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
     const uint32_t w = threadIdx.x >> 6;
     if (!grouped || gridDim.x < 8) return {(uint64_t)blockIdx.x * 4 + w, n_tasks, (uint64_t)gridDim.x * 4};
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena,
     const uint32_t lterm = len_term(len);
     const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
     const uint64_t n_tasks = (n + run - 1) / run;
-    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kNoXcdGroups) == 0);
+    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kXcdGroups) != 0);
     for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
         const uint64_t p0 = task * run;
         const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
@@ -355,7 +357,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
     __shared__ RaggedTileLds s_tile[4];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RaggedTileLds& t = s_tile[w];
-    const TaskRange tr = xcd_tasks((n + 63) / 64, (kflags & kNoXcdGroups) == 0);
+    const TaskRange tr = xcd_tasks((n + 63) / 64, (kflags & kXcdGroups) != 0);
     uint64_t tile = tr.first;
     pipck_desc dn = pipck_desc{0, 0, 0};
     if (tile < tr.end && tile * 64 + lane < n) dn = desc[tile * 64 + lane];
@@ -575,10 +577,10 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // rows in flight per wave: 16 for jumbo packets, 8 below 4 KiB (measured, profiles/README.md)
         const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (cpp >= 256 ? 16u : 8u);
         const FlatVariant* fv = &flat_variant(loads);
-        // a wave task covers ~32 rows of 1 KiB and the grid holds one task per wave
-        // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_grid_scan*.jsonl)
+        // a wave task covers ~64 rows of 1 KiB and the grid holds one task per wave
+        // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)
         const uint32_t flags = g_tune.flags.load();
-        const uint32_t rows = (flags >> 8) ? (flags >> 8) : 32u;
+        const uint32_t rows = (flags >> 8) ? (flags >> 8) : 64u;
         const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);

@@ -54,17 +54,16 @@ def main():
                 nbytes = (w.length + 2) * n
                 run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             res = {}
-            arms = {"static": {}, "no_xcd": {"xcd_groups": False}, "rows_16": {"rows_per_task": 16},
-                    "no_xcd_rows_64": {"xcd_groups": False, "rows_per_task": 64}}
+            arms = {"default": {}, "xcd_groups": {"xcd_groups": True}, "rows_32": {"rows_per_task": 32},
+                    "rows_128": {"rows_per_task": 128}}
             if w.ragged:
-                arms = {"static": {}, "uncapped": {"blocks": 1 << 30},
-                        "uncapped_no_xcd": {"blocks": 1 << 30, "xcd_groups": False}}
+                arms = {"default": {}, "xcd_groups": {"xcd_groups": True}, "grid_16384": {"blocks": 16384}}
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
                     res.setdefault(xcd, []).append(timed(run, a.iters))
                     out = run()
-                    if xcd == "static":
+                    if xcd == "default":
                         ref = out.clone()
                     else:
                         assert torch.equal(out, ref)
