@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# SQ instruction-mix counters (one pass, counters only) for a bench workload:
+#   WL=cfg4 bash tools/sq_profile.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+WL="${WL:-cfg4}"
+OUT="gpurun_out/sq_${WL}"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+    SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES -d "$OUT/pmc" -o run --output-format csv -- \
+    python3 bench.py --workload "$WL" --no-cpu --steps 2 --warmup 1 > "$OUT/bench.json" 2> "$OUT/err.log"
+rc=$?
+tail -2 "$OUT/err.log"
+exit $rc
