@@ -37,19 +37,31 @@ __device__ __forceinline__ uint32_t fold32(uint32_t x) { return (x & 0xFFFFu) + 
 __device__ __forceinline__ uint32_t fold16(uint32_t x) { return fold32(fold32(x)); }
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | (x >> 8); }
 
-// Keep bytes [lo, hi) of a 16-byte chunk (0 <= lo, hi <= 16).
-__device__ __forceinline__ uint32_t byte_window(int lo, int hi, int k) {
-    int a = min(max(lo - 4 * k, 0), 4), b = min(max(hi - 4 * k, 0), 4);
-    uint32_t mb = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
-    uint32_t ma = a >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a)) - 1u);
-    return mb & ~ma;
+// Byte masks of a 16-byte chunk as two little-endian u64 halves.  The low n
+// bytes (n clamped to [0, 16]) are ~0 >> (64 - 8k) per half -- one 64-bit
+// shift each; k == 0 is selected explicitly because a shift by 64 wraps.
+struct Mask128 {
+    uint64_t m0, m1;
+};
+__device__ __forceinline__ uint64_t low_bytes64(int k) {  // k in [0, 8]
+    return k > 0 ? (~0ull >> (64 - 8 * k)) : 0ull;
 }
-__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi) {
-    v.x &= byte_window(lo, hi, 0);
-    v.y &= byte_window(lo, hi, 1);
-    v.z &= byte_window(lo, hi, 2);
-    v.w &= byte_window(lo, hi, 3);
+__device__ __forceinline__ Mask128 low_bytes(int n) {
+    return {low_bytes64(min(max(n, 0), 8)), low_bytes64(min(max(n - 8, 0), 8))};
+}
+__device__ __forceinline__ u32x4 and_mask(u32x4 v, Mask128 m) {
+    v.x &= (uint32_t)m.m0;
+    v.y &= (uint32_t)(m.m0 >> 32);
+    v.z &= (uint32_t)m.m1;
+    v.w &= (uint32_t)(m.m1 >> 32);
     return v;
+}
+// Keep bytes [0, hi) of a chunk: a segment's last chunk.
+__device__ __forceinline__ u32x4 mask_tail(u32x4 v, int hi) { return and_mask(v, low_bytes(hi)); }
+// Keep bytes [lo, hi) of a chunk (0 <= lo; hi may lie outside [0, 16]).
+__device__ __forceinline__ u32x4 mask_chunk(u32x4 v, int lo, int hi) {
+    const Mask128 a = low_bytes(hi), b = low_bytes(lo);
+    return and_mask(v, Mask128{a.m0 & ~b.m0, a.m1 & ~b.m1});
 }
 
 __device__ __forceinline__ uint64_t sum4(u32x4 v) {

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict_
         for (uint32_t c = threadIdx.x; c < nch; c += blockDim.x) {
             u32x4 v = base[c];
             const int hi = (int)r.len - 16 * (int)c;
-            if (hi < 16) v = mask_chunk(v, 0, hi);
+            if (hi < 16) v = mask_tail(v, hi);
 #pragma unroll
             for (int k = 0; k < 4; k++) {  // offsets within the segment: 4k+0, 4k+2 even; 4k+1, 4k+3 odd
                 const uint32_t x = v[k];

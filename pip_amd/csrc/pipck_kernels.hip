@@ -90,7 +90,8 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
                 const int lo = c == 0 ? head : 0;
                 const int hi = end - 16 * c;
                 u32x4 x = v[k];
-                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+                if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
+                else if (hi < 16) x = mask_tail(x, hi);
                 acc += sum4(x);
             }
         }
@@ -213,7 +214,7 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
             uint32_t k = pp.k + lane;
             if (k >= cpp) k -= cpp;
             u32x4 x = v[u];
-            if (k == nch - 1 && tail < 16) x = mask_chunk(x, 0, tail);
+            if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
             const uint64_t val = sum4(x);
             const uint32_t b = cpp - pp.k;  // first lane holding the next packet
             if (b >= 64 || pp.pkt + 1 >= np) {
@@ -337,7 +338,8 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
         const int lo = rel == 0 ? (int)(span & 15) : 0;
         const int hi = (int)(span >> 4) - 16 * rel;
         u32x4 x = v[u];
-        if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+        if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
+        else if (hi < 16) x = mask_tail(x, hi);
         const uint32_t val = active ? fold64(sum4(x)) : 0u;
         const uint32_t inc = wave_incl_scan(val);
         const bool last_chunk = hi <= 16;  // this chunk ends its segment
