@@ -120,6 +120,26 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
 int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
                         const uint32_t* d_pseudo, uint8_t* d_ok, uint32_t* d_err, void* stream);
 
+/* Incremental update for header rewrites (RFC 1624, SURVEY.md section 8 f4;
+ * replaces a full re-run of pip_standard_checksum, pip_checksum.cpp:13-33,
+ * after a field change).  Packet i at a = d_arena + i*stride carries pip's
+ * checksum of the covered bytes a[cover_off, cover_off+cover_len) (an IPv4
+ * header, or an L4 segment with flow pseudo-headers) as the big-endian u16 at
+ * a + ck_off (htons(result), as pip's callers store it).  Bytes
+ * a[edit_off, edit_off+edit_len) are replaced by d_new + i*new_stride, and
+ * when d_pseudo_old / d_pseudo_new are given (prepared bases of the old and
+ * new flow tables, e.g. a NAT address rewrite) the pseudo-header changes too;
+ * the field is patched as  ~(~HC + ~m + m')  -- RFC 1624 eqn. 3.  The result
+ * equals pip's full recomputation bit for bit (the 0x0000/0xFFFF corner eqn.
+ * 3 cannot decide alone is settled by scanning that packet).
+ * PIPCK_EINVAL unless: checksum field and edit lie in the cover at even
+ * offsets from cover_off and do not overlap; edit_len is even or the edit
+ * ends the cover; cover_off + cover_len <= stride; cover_len <= 65535. */
+int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint32_t cover_off, uint32_t cover_len,
+                       uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new,
+                       uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
+                       uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, void* stream);
+
 /* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
  * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows

@@ -49,6 +49,8 @@ SIGNATURES = {
     "pipck_checksum_chains": (_i32, [_p, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p]),
     "pipck_verify_fixed": (_i32, [_p, _u64, _u32, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_verify_ragged": (_i32, [_p, _p, _u64, _p, _p, _p, _p]),
+    "pipck_update_fixed": (_i32, [_p, _u64, _u64, _u32, _u32, _u32, _u32, _u32, _p, _u64, _p, _p, _u32, _p, _u64,
+                                  _p]),
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
     "pipck_cfg_seed": (_u64, [_u32]),
     "pipck_gen_fixed": (_i32, [_p, _u64, _u32, _u64, _u64, _u64, _u32, _p]),

@@ -294,37 +294,58 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 }
 
 struct RaggedTileLds {
-    uint32_t pre[64];   // exclusive chunk prefix of the tile's segments
+    uint64_t base[64];  // 16-byte-aligned base address of each segment
+    uint32_t pre[65];   // exclusive chunk prefix of the tile's segments; pre[64] = total
     uint32_t acc[64];   // LE residue partial per segment
     uint32_t span[64];  // (end << 4) | head, relative to the 16-byte-aligned base
-    uint64_t base[64];  // 16-byte-aligned base address of each segment
 };
 
-// Map U rows of the tile's chunk stream to segments (binary search over the
-// chunk prefix: the last segment starting at or before the chunk, which skips
-// empty segments) and issue their 16-byte loads.
+constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
+
+// Map U rows of the tile's chunk stream to segments and issue their 16-byte
+// loads.  A lane's chunk advances by 64 per row, so it usually stays in the
+// segment it held a row earlier (one LDS compare against that segment's end);
+// only lanes that crossed a boundary binary-search the chunk prefix for the
+// last segment starting at or before the chunk, which skips empty segments.
 template <int U, bool NT>
 __device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
-                                             u32x4 (&v)[U], uint32_t (&sx)[U]) {
+                                             u32x4 (&v)[U], uint32_t (&sx)[U], uint32_t& scur) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t c = c0 + u * 64 + lane;
-        uint32_t s = 0;
+        uint32_t s = scur;
+        if (c >= t.pre[s + 1]) {
+            s = 0;
 #pragma unroll
-        for (int st = 32; st > 0; st >>= 1)
-            if (t.pre[s + st] <= c) s += st;
+            for (int st = 32; st > 0; st >>= 1)
+                if (t.pre[s + st] <= c) s += st;
+        }
+        scur = s;
         sx[u] = s;
         const u32x4* p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
         v[u] = c < total ? (NT ? load_stream(p) : load_plain(p)) : u32x4{0u, 0u, 0u, 0u};
     }
 }
 
-// Reduce U rows by segment: a wave prefix scan per row; the lane holding a
-// segment's last chunk in the row adds (its prefix - the prefix just before
-// the segment's first chunk in the row) to the segment's LDS partial.
+// Add a run of whole rows of one segment (per-lane partials in racc) to the
+// segment's LDS partial: one wave sum, one LDS add.
+__device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_t& racc, uint32_t& rseg) {
+    if (rseg == kNoSeg) return;  // wave-uniform
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(racc), 63);
+    if (lane == 0) atomicAdd(&t.acc[rseg], tot);
+    racc = 0;
+    rseg = kNoSeg;
+}
+
+// Reduce U rows by segment.  A row lying wholly inside one segment (most rows
+// of multi-KiB packets) only adds into the per-lane run partial racc.  Any
+// other row takes a wave prefix scan: the lane holding a segment's last chunk
+// in the row adds (its prefix - the prefix just before the segment's first
+// chunk in the row) to the segment's LDS partial.
 template <int U>
 __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
-                                              const u32x4 (&v)[U], const uint32_t (&sx)[U]) {
+                                              const u32x4 (&v)[U], const uint32_t (&sx)[U], uint32_t& racc,
+                                              uint32_t& rseg) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t row = c0 + u * 64;
@@ -341,6 +362,16 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
         if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
         else if (hi < 16) x = mask_tail(x, hi);
         const uint32_t val = active ? fold64(sum4(x)) : 0u;
+        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+        if (t.pre[s0 + 1] >= row + 64) {  // the whole row is in segment s0 (pre[64] = total)
+            if (s0 != rseg) {
+                ragged_flush(t, lane, racc, rseg);
+                rseg = s0;
+            }
+            racc += val;
+            continue;
+        }
+        ragged_flush(t, lane, racc, rseg);
         const uint32_t inc = wave_incl_scan(val);
         const bool last_chunk = hi <= 16;  // this chunk ends its segment
         const bool tail = active && (lane == 63 || last_chunk);
@@ -378,20 +409,22 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         const uint32_t incl = wave_incl_scan(nch);
         const uint32_t total = __shfl(incl, 63, 64);
         t.pre[lane] = incl - nch;
+        if (lane == 63) t.pre[64] = incl;
         t.span[lane] = ((head + len) << 4) | head;
         t.base[lane] = addr - head;
         t.acc[lane] = 0;
         wave_sync();
         u32x4 v[U];
         uint32_t sx[U];
-        if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx);
+        uint32_t scur = 0, racc = 0, rseg = kNoSeg;
+        if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur);
         for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
             const bool more = c0 + 64 * U < total;  // wave-uniform
             if (PIPE) {
                 u32x4 nv[U];
                 uint32_t nsx[U];
-                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx);
-                ragged_reduce<U>(t, c0, total, lane, v, sx);
+                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx, scur);
+                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg);
                 if (more) {
 #pragma unroll
                     for (int u = 0; u < U; u++) {
@@ -400,10 +433,11 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
                     }
                 }
             } else {
-                ragged_reduce<U>(t, c0, total, lane, v, sx);
-                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx);
+                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg);
+                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur);
             }
         }
+        ragged_flush(t, lane, racc, rseg);
         wave_sync();
         if (valid) {
             const uint32_t F = bad ? 0u : be_fold(t.acc[lane], addr);

@@ -125,6 +125,20 @@ def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None
     return out
 
 
+def update_fixed(arena, stride: int, n: int, cover_off: int, cover_len: int, ck_off: int, edit_off: int,
+                 edit_len: int, new_bytes=None, new_stride: int = 0, pseudo_old=None, pseudo_new=None,
+                 n_flows: int = 1, flow_of=None, flow_origin: int = 0) -> None:
+    """Rewrite bytes [edit_off, edit_off+edit_len) of every packet with new_bytes[i*new_stride:] and patch
+    the big-endian checksum field at ck_off incrementally (RFC 1624); see pipck_update_fixed."""
+    _check_span(arena, stride, cover_off + cover_len, n)
+    if edit_len and new_bytes is not None and n and \
+            (n - 1) * new_stride + edit_len > new_bytes.numel() * new_bytes.element_size():
+        raise ValueError("new_bytes is too small for the batch")
+    call("pipck_update_fixed", _ptr(arena), stride, n, cover_off, cover_len, ck_off, edit_off, edit_len,
+         _ptr(new_bytes), new_stride, _ptr(pseudo_old), _ptr(pseudo_new), n_flows, _ptr(flow_of), flow_origin,
+         current_stream(arena.device))
+
+
 def _check_span(arena, stride, length, n):
     """Host-side guard: the kernels must never read past the arena."""
     if n and (n - 1) * stride + length > arena.numel() * arena.element_size():

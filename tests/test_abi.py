@@ -106,3 +106,23 @@ def test_batch_abi_rejects_out_of_domain_arguments():
     rc = lib.pipck_checksum_fixed(None, 16, 16, 1, None, 1, None, 0, C.c_void_p(16), None)
     assert rc == _lib.PIPCK_EINVAL
     assert lib.pipck_checksum_fixed(None, 16, 16, 0, None, 1, None, 0, None, None) == _lib.PIPCK_OK
+
+
+@pytest.mark.parametrize("args,why", [
+    # (stride, cover_off, cover_len, ck_off, edit_off, edit_len, pseudo_old, pseudo_new)
+    ((24, 0, 20, 11, 12, 4, None, None), "odd checksum offset"),
+    ((24, 0, 20, 10, 13, 4, None, None), "odd edit offset"),
+    ((24, 0, 20, 10, 12, 3, None, None), "odd edit inside the cover"),
+    ((24, 0, 20, 10, 8, 4, None, None), "edit overlaps the field"),
+    ((24, 0, 20, 10, 18, 4, None, None), "edit past the cover"),
+    ((24, 6, 20, 10, 12, 4, None, None), "cover past the stride"),
+    ((24, 0, 20, 10, 12, 4, C.c_void_p(16), None), "one pseudo table"),
+    ((70000, 0, 65536, 10, 12, 4, None, None), "cover_len out of domain"),
+])
+def test_update_rejects_bad_geometry(args, why):
+    lib = _lib.load()
+    stride, cover_off, cover_len, ck_off, edit_off, edit_len, po, pn = args
+    rc = lib.pipck_update_fixed(C.c_void_p(16), stride, 1, cover_off, cover_len, ck_off, edit_off, edit_len,
+                                C.c_void_p(16), 8, po, pn, 1, None, 0, None)
+    assert rc == _lib.PIPCK_EINVAL, why
+    assert b"pipck_update_fixed" in lib.pipck_last_error()

@@ -57,7 +57,7 @@ def main():
             arms = {"default": {}, "xcd_groups": {"xcd_groups": True}, "rows_32": {"rows_per_task": 32},
                     "rows_128": {"rows_per_task": 128}}
             if w.ragged:
-                arms = {"default": {}, "xcd_groups": {"xcd_groups": True}, "grid_16384": {"blocks": 16384}}
+                arms = {"default": {}, "loads_2": {"loads_per_lane": 2}, "loads_8": {"loads_per_lane": 8}, "pipe_4": {"loads_per_lane": 5}}
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
