@@ -83,8 +83,15 @@ __device__ __forceinline__ uint16_t finish(uint32_t pseudo_total, uint32_t be_su
     return (uint16_t)~fold16(pseudo_total + be_sum);
 }
 
+// Arena loads are issued in the global address space explicitly.  A pointer
+// rebuilt from an integer (the ragged kernel's LDS segment bases) is otherwise
+// generic, and a FLAT load counts against LGKM_CNT as well as VM_CNT: every
+// later s_waitcnt lgkmcnt(0) for an LDS read would then also wait for the
+// outstanding HBM loads, serialising the rows in flight.
+typedef __attribute__((address_space(1))) const u32x4 global_u32x4;
+__device__ __forceinline__ const global_u32x4* as_global(const u32x4* p) { return (const global_u32x4*)p; }
 // Non-temporal 16-byte load: the arena is streamed exactly once.
-__device__ __forceinline__ u32x4 load_stream(const u32x4* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ u32x4 load_plain(const u32x4* p) { return *p; }
+__device__ __forceinline__ u32x4 load_stream(const u32x4* p) { return __builtin_nontemporal_load(as_global(p)); }
+__device__ __forceinline__ u32x4 load_plain(const u32x4* p) { return *as_global(p); }
 
 }  // namespace pipck

@@ -130,13 +130,16 @@ struct TaskRange {
     uint64_t first, end, step;
 };
 constexpr uint32_t kXcdGroups = 8u;
+constexpr uint32_t kNoPackedTiles = 16u;  // pipck_tune flags bit 4: ragged tiles always take the lookup path
+constexpr uint32_t kWideBlocks = 32u;     // pipck_tune flags bit 5: 4-wave ragged blocks instead of 1-wave
+template <uint32_t WPB = 4>  // waves per block
 __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
     const uint32_t w = threadIdx.x >> 6;
-    if (!grouped || gridDim.x < 8) return {(uint64_t)blockIdx.x * 4 + w, n_tasks, (uint64_t)gridDim.x * 4};
+    if (!grouped || gridDim.x < 8) return {(uint64_t)blockIdx.x * WPB + w, n_tasks, (uint64_t)gridDim.x * WPB};
     const uint32_t g = blockIdx.x & 7, gi = blockIdx.x >> 3;
     const uint32_t nb = (gridDim.x - g + 7) >> 3;  // blocks in group g
     const uint64_t b = n_tasks * g / 8, e = n_tasks * (g + 1) / 8;
-    return {b + (uint64_t)gi * 4 + w, e, (uint64_t)nb * 4};
+    return {b + (uint64_t)gi * WPB + w, e, (uint64_t)nb * WPB};
 }
 
 // ---------------------------------------------------------------------------
@@ -148,6 +151,11 @@ __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
 // wave, and since a packet spans >= 64 chunks a row holds at most one packet
 // boundary.  Lanes keep a running u64 sum for the packet the row is in; at a
 // boundary the finished packet's partials are folded and wave-reduced once.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -276,11 +284,6 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena,
 // ---------------------------------------------------------------------------
 // ragged / chain-segment kernel
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
 // Inclusive wave-64 prefix sum on the DPP crossbar (GFX9 DPP: row_shr inside
 // 16-lane rows, then row_bcast:15 / row_bcast:31 across rows) -- no LDS trips.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -302,28 +305,54 @@ struct RaggedTileLds {
 
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
 
-// Map U rows of the tile's chunk stream to segments and issue their 16-byte
-// loads.  A lane's chunk advances by 64 per row, so it usually stays in the
-// segment it held a row earlier (one LDS compare against that segment's end);
-// only lanes that crossed a boundary binary-search the chunk prefix for the
-// last segment starting at or before the chunk, which skips empty segments.
+// Lane 0's value of a 64-bit quantity, as a scalar (both halves zero-extended).
+__device__ __forceinline__ uint64_t first_lane_u64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Segment of chunk c: the last segment starting at or before c (which skips
+// empty segments).  A lane's chunk advances by 64 per row, so it usually stays
+// in the segment it held a row earlier (one LDS compare against that
+// segment's end); only lanes that crossed a boundary binary-search the prefix.
+__device__ __forceinline__ uint32_t ragged_seg_of(const RaggedTileLds& t, uint32_t c, uint32_t& scur) {
+    uint32_t s = scur;
+    if (c >= t.pre[s + 1]) {
+        s = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+            if (t.pre[s + st] <= c) s += st;
+    }
+    scur = s;
+    return s;
+}
+
+// Issue the 16-byte loads of U rows of the tile's chunk stream.  A packed tile
+// (segments back to back at 16-byte granularity, see k_ragged) addresses chunk
+// c directly at tbase + 16c, so its loads wait on nothing; otherwise each
+// lane's segment is looked up first to find its base.
 template <int U, bool NT>
 __device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
-                                             u32x4 (&v)[U], uint32_t (&sx)[U], uint32_t& scur) {
+                                             u32x4 (&v)[U], uint32_t (&sx)[U], uint32_t& scur, bool packed,
+                                             uintptr_t tbase) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t c = c0 + u * 64 + lane;
-        uint32_t s = scur;
-        if (c >= t.pre[s + 1]) {
-            s = 0;
-#pragma unroll
-            for (int st = 32; st > 0; st >>= 1)
-                if (t.pre[s + st] <= c) s += st;
+        // Lanes past the tile's last chunk re-read that chunk (same cache line
+        // as a live lane; ragged_reduce ignores them): the loads stay
+        // unconditional, so the reduce can wait for each row alone (vmcnt(N))
+        // instead of draining the whole batch at a branch join.
+        const uint32_t c = min(c0 + u * 64 + lane, total - 1);
+        const u32x4* p;
+        if (packed) {
+            p = reinterpret_cast<const u32x4*>(tbase) + c;
+        } else {
+            const uint32_t s = ragged_seg_of(t, c, scur);
+            sx[u] = s;
+            p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
         }
-        scur = s;
-        sx[u] = s;
-        const u32x4* p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
-        v[u] = c < total ? (NT ? load_stream(p) : load_plain(p)) : u32x4{0u, 0u, 0u, 0u};
+        v[u] = NT ? load_stream(p) : load_plain(p);
+        __builtin_amdgcn_sched_barrier(0);  // keep row order (see flat_load_rows)
     }
 }
 
@@ -345,14 +374,14 @@ __device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_
 template <int U>
 __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
                                               const u32x4 (&v)[U], const uint32_t (&sx)[U], uint32_t& racc,
-                                              uint32_t& rseg) {
+                                              uint32_t& rseg, bool packed, uint32_t& scur) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t row = c0 + u * 64;
         if (row >= total) continue;  // wave-uniform
         const uint32_t c = row + lane;
         const bool active = c < total;
-        const uint32_t s = sx[u];
+        const uint32_t s = packed ? ragged_seg_of(t, c, scur) : sx[u];
         const uint32_t pre = t.pre[s];
         const uint32_t span = t.span[s];
         const int rel = (int)(c - pre);
@@ -363,7 +392,9 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
         else if (hi < 16) x = mask_tail(x, hi);
         const uint32_t val = active ? fold64(sum4(x)) : 0u;
         const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
-        if (t.pre[s0 + 1] >= row + 64) {  // the whole row is in segment s0 (pre[64] = total)
+        const uint32_t end0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.pre[s0 + 1]);
+        rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
+        if (end0 >= row + 64) {  // the whole row is in segment s0 (pre[64] = total); wave-uniform
             if (s0 != rseg) {
                 ragged_flush(t, lane, racc, rseg);
                 rseg = s0;
@@ -381,16 +412,55 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
     }
 }
 
-template <bool FINAL, int U, bool PIPE, bool NT>
+// Stream a tile's chunks U rows at a time and reduce them by segment.
+template <int U, bool PIPE, bool NT, bool PACKED>
+__device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, int lane, uintptr_t tbase,
+                                              uint32_t& racc, uint32_t& rseg) {
+    u32x4 v[U];
+    uint32_t sx[U];
+    uint32_t scur = 0, rcur = 0;
+    if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur, PACKED, tbase);
+    for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
+        const bool more = c0 + 64 * U < total;  // wave-uniform
+        if (PIPE) {
+            u32x4 nv[U];
+            uint32_t nsx[U];
+            if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx, scur, PACKED, tbase);
+            ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, PACKED, rcur);
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    v[u] = nv[u];
+                    sx[u] = nsx[u];
+                }
+            }
+        } else {
+            ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, PACKED, rcur);
+            if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
+        }
+    }
+}
+
+// One tile per wave, and by default one wave per block: tiles differ in size,
+// and a block's slot (and LDS) is only released when its slowest wave ends, so
+// 4-wave blocks idle ~a quarter of the wave slots on Zipf-sized traffic.
+template <bool FINAL, int U, bool PIPE, bool NT, uint32_t WPB>
 __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ arena, const pipck_desc* __restrict__ desc,
                                                 uint64_t n, const uint32_t* __restrict__ pseudo,
                                                 uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
                                                 uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
                                                 uint32_t kflags) {
-    __shared__ RaggedTileLds s_tile[4];
+    __shared__ RaggedTileLds s_tile[WPB];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RaggedTileLds& t = s_tile[w];
-    const TaskRange tr = xcd_tasks((n + 63) / 64, (kflags & kXcdGroups) != 0);
+    const uint32_t tpw = (kflags >> 16) & 0xFFu;  // consecutive tiles per wave (0: one window, see xcd_tasks)
+    TaskRange tr;
+    if (tpw) {
+        const uint64_t first = ((uint64_t)blockIdx.x * WPB + w) * tpw;
+        tr = {first, min(first + tpw, (n + 63) / 64), 1};
+    } else {
+        tr = xcd_tasks<WPB>((n + 63) / 64, (kflags & kXcdGroups) != 0);
+    }
     uint64_t tile = tr.first;
     pipck_desc dn = pipck_desc{0, 0, 0};
     if (tile < tr.end && tile * 64 + lane < n) dn = desc[tile * 64 + lane];
@@ -413,30 +483,19 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         t.span[lane] = ((head + len) << 4) | head;
         t.base[lane] = addr - head;
         t.acc[lane] = 0;
+        // Packed tile: every segment starts 16-byte aligned right where the
+        // previous one's chunks end (the layout of pip's TX batches and of the
+        // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
+        const uint64_t next_off = (uint64_t)__shfl_down((long long)d.offset, 1, 64);
+        const bool link = lane == 63 || seg + 1 >= n || d.offset + 16ull * nch == next_off;
+        const bool packed = (kflags & kNoPackedTiles) == 0 && __all(head == 0 && link);
+        const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
         wave_sync();
-        u32x4 v[U];
-        uint32_t sx[U];
-        uint32_t scur = 0, racc = 0, rseg = kNoSeg;
-        if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur);
-        for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
-            const bool more = c0 + 64 * U < total;  // wave-uniform
-            if (PIPE) {
-                u32x4 nv[U];
-                uint32_t nsx[U];
-                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx, scur);
-                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg);
-                if (more) {
-#pragma unroll
-                    for (int u = 0; u < U; u++) {
-                        v[u] = nv[u];
-                        sx[u] = nsx[u];
-                    }
-                }
-            } else {
-                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg);
-                if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur);
-            }
-        }
+        uint32_t racc = 0, rseg = kNoSeg;
+        if (packed)
+            ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, racc, rseg);
+        else  // fewer rows in flight: the lookup path needs a segment register per row
+            ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, racc, rseg);
         ragged_flush(t, lane, racc, rseg);
         wave_sync();
         if (valid) {
@@ -616,7 +675,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // a wave task covers ~64 rows of 1 KiB and the grid holds one task per wave
         // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)
         const uint32_t flags = g_tune.flags.load();
-        const uint32_t rows = (flags >> 8) ? (flags >> 8) : 64u;
+        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 64u;
         const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
@@ -635,17 +694,34 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     return PIPCK_OK;
 }
 
+template <bool FINAL, int U, bool PIPE, bool NT>
+static void launch_ragged_k(bool wide, uint64_t tiles, hipStream_t s, const uint8_t* a, const pipck_desc* d,
+                            uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint8_t* ok, uint32_t* err,
+                            uint32_t f) {
+    // one tile per wave: the in-order dispatcher hands out tiles as waves finish
+    // (measured best, profiles/r01_size_scan*.jsonl)
+    const uint32_t tpw = (f >> 16) & 0xFFu;
+    const uint64_t waves = tpw ? (tiles + tpw - 1) / tpw : tiles;
+    if (wide)
+        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(tpw ? (uint32_t)((waves + 3) / 4) : grid_for(4, tiles, 0)),
+                           dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+    else
+        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(tpw ? (uint32_t)waves : grid_for(1, tiles, 0)),
+                           dim3(64), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+}
+
 template <int U, bool PIPE>
-static void launch_ragged_u(bool final_, bool nt, dim3 grid, hipStream_t s, const uint8_t* a, const pipck_desc* d,
-                            uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint8_t* ok,
-                            uint32_t* err) {
+static void launch_ragged_u(bool final_, bool nt, uint64_t tiles, hipStream_t s, const uint8_t* a,
+                            const pipck_desc* d, uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg,
+                            uint8_t* ok, uint32_t* err) {
     const uint32_t f = g_tune.flags.load();
+    const bool wide = (f & kWideBlocks) != 0;
     if (final_) {
-        if (nt) hipLaunchKernelGGL((k_ragged<true, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
-        else hipLaunchKernelGGL((k_ragged<true, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+        if (nt) launch_ragged_k<true, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
+        else launch_ragged_k<true, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
     } else {
-        if (nt) hipLaunchKernelGGL((k_ragged<false, U, PIPE, true>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
-        else hipLaunchKernelGGL((k_ragged<false, U, PIPE, false>), grid, dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+        if (nt) launch_ragged_k<false, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
+        else launch_ragged_k<false, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
     }
 }
 
@@ -653,20 +729,19 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint8_t* d_ok, uint32_t* d_err,
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
-    // one tile per wave: the in-order dispatcher hands out tiles as waves finish
-    // (measured best, profiles/r01_size_scan*.jsonl)
-    const dim3 grid(grid_for(4, tiles, 0));
-    // loads_per_lane: 2/4/8 rows in flight, 3/5/9 = pipelined 2/4/8 (default: 4)
+    // loads_per_lane: 2/4/8/16 rows in flight on packed tiles (at most 4 on
+    // others), 3/5/9 = pipelined 2/4/8 (default: 4)
     const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 4u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {
-        case 2: launch_ragged_u<2, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 4: launch_ragged_u<4, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 8: launch_ragged_u<8, false>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 3: launch_ragged_u<2, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 9: launch_ragged_u<8, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        default: launch_ragged_u<4, true>(final_, nt, grid, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 2: launch_ragged_u<2, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 4: launch_ragged_u<4, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 8: launch_ragged_u<8, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 16: launch_ragged_u<16, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 3: launch_ragged_u<2, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 9: launch_ragged_u<8, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        default: launch_ragged_u<4, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
     }
     PIPCK_LAUNCHED("k_ragged");
     return PIPCK_OK;

@@ -283,9 +283,10 @@ def test_ragged_vs_oracle(oracle, n):
 @pytest.mark.parametrize("blocks", [1, 3, 8, 9, 17])
 @pytest.mark.parametrize("xcd", [True, False])
 @pytest.mark.parametrize("rows", [2, 4, 8, 3, 5, 9])
-def test_ragged_launch_shapes(oracle, blocks, xcd, rows):
-    """Every ragged row depth (plain and pipelined), grids smaller and larger
-    than the 8 XCD groups, tiles left over after the groups split."""
+@pytest.mark.parametrize("wide", [False, True])
+def test_ragged_launch_shapes(oracle, blocks, xcd, rows, wide):
+    """Every ragged row depth (plain and pipelined), 1- and 4-wave blocks, grids
+    smaller and larger than the 8 XCD groups, tiles left over after the split."""
     rng = np.random.default_rng(blocks * 100 + rows * 2 + xcd)
     n = 64 * 23 + 5
     offs, lens, size = _ragged_case(rng, n, 3000)
@@ -293,12 +294,53 @@ def test_ragged_launch_shapes(oracle, blocks, xcd, rows):
     _, arena = upload(host, 0)
     _, pseudo = engine.gen_flows(4, N_FLOWS, 7, 6)
     desc = engine.make_desc(offs, lens, np.arange(n) % N_FLOWS)
-    engine.tune(0, rows, blocks, xcd_groups=xcd)
+    engine.tune(0, rows, blocks, xcd_groups=xcd, wide_blocks=wide)
     try:
         got = u16(engine.checksum_ragged(arena, desc, pseudo))
     finally:
         engine.tune()
     assert np.array_equal(got, oracle.batch_ragged(host, offs, lens, 4, 6, 7, N_FLOWS, 0))
+
+
+def _packed_case(rng, n, max_len=3000):
+    """Segments back to back at 16-byte granularity (packed tiles), with some
+    tiles broken on purpose: a 16-byte gap, a misaligned tile, empty and odd
+    segments.  Padding bytes are random, so tail masking is exercised."""
+    lens = rng.integers(0, max_len + 1, n).astype(np.uint32)
+    lens[rng.random(n) < 0.05] = 0
+    lens[rng.random(n) < 0.2] |= 1
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 16
+    for i in range(n):
+        tile = i // 64
+        if tile % 5 == 3 and i % 64 == 17:
+            pos += 16                      # a gap: tile not packed
+        if tile % 7 == 4 and i % 64 == 0:
+            pos += 1                       # a misaligned tile: not packed
+        elif i % 64 == 0:
+            pos = (pos + 15) & ~15
+        offs[i] = pos
+        pos += (int(lens[i]) + 15) & ~15 if tile % 7 != 4 else int(lens[i])
+    return offs, lens, pos + 16
+
+
+@pytest.mark.parametrize("rows", [4, 8, 5])
+def test_ragged_packed_tiles(oracle, rows):
+    rng = np.random.default_rng(rows)
+    n = 64 * 40 + 9
+    offs, lens, size = _packed_case(rng, n)
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    _, arena = upload(host, 0)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, 7, 6)
+    desc = engine.make_desc(offs, lens, np.arange(n) % N_FLOWS)
+    want = oracle.batch_ragged(host, offs, lens, 4, 6, 7, N_FLOWS, 0)
+    try:
+        for packed in (True, False):
+            engine.tune(0, rows, packed_tiles=packed)
+            got = u16(engine.checksum_ragged(arena, desc, pseudo))
+            assert np.array_equal(got, want), f"packed_tiles={packed}"
+    finally:
+        engine.tune()
 
 
 def test_ragged_out_of_domain_flags_error(oracle):

@@ -54,10 +54,11 @@ def main():
                 nbytes = (w.length + 2) * n
                 run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
             res = {}
-            arms = {"default": {}, "xcd_groups": {"xcd_groups": True}, "rows_32": {"rows_per_task": 32},
+            arms = {"default": {}, "loads_8": {"loads_per_lane": 8}, "pipe_8": {"loads_per_lane": 9}, "pipe_4": {"loads_per_lane": 5},
                     "rows_128": {"rows_per_task": 128}}
             if w.ragged:
-                arms = {"default": {}, "loads_2": {"loads_per_lane": 2}, "loads_8": {"loads_per_lane": 8}, "pipe_4": {"loads_per_lane": 5}}
+                arms = {"default": {}, "wide_blocks": {"wide_blocks": True}, "loads_8": {"loads_per_lane": 8},
+                        "pipe_4": {"loads_per_lane": 5}, "loads_2": {"loads_per_lane": 2}}
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
