@@ -162,14 +162,25 @@ __device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
     return s;
 }
 
-template <bool VERIFY>
-__device__ __forceinline__ void flat_finish(uint64_t acc, uint64_t pkt, uint32_t flow, const uint32_t* pseudo,
-                                            const uint32_t* flow_of, uint32_t lterm, uint16_t* out, uint8_t* ok,
-                                            int lane) {
+// A finished packet's folded big-endian sum goes to the wave's LDS slot; the
+// pseudo-header loads and the global stores wait for the task's end
+// (flat_write): on gfx9 both count in VM_CNT, so inside the row loop each
+// one would make the next row's wait drain every load in flight.
+constexpr uint32_t kFlatMaxRun = 128;  // packets per wave task
+__device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint32_t* res, int lane) {
     const uint32_t s = wave_reduce_add(fold64(acc));
-    if (lane == 0) {
-        const uint32_t F = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
-        const uint32_t P = pseudo ? pseudo[flow_of ? flow_of[pkt] : flow] + lterm : 0u;
+    if (lane == 0) res[i] = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
+}
+
+template <bool VERIFY>
+__device__ __forceinline__ void flat_write(const uint32_t* res, uint64_t p0, uint32_t np, const uint32_t* pseudo,
+                                           uint32_t n_flows, const uint32_t* flow_of, uint64_t flow_origin,
+                                           uint32_t lterm, uint16_t* out, uint8_t* ok, int lane) {
+    for (uint32_t i = lane; i < np; i += 64) {
+        const uint64_t pkt = p0 + i;
+        const uint32_t F = res[i];
+        uint32_t P = 0;
+        if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)] + lterm;
         if (VERIFY)
             ok[pkt] = fold16(P + F) == 0xFFFFu;
         else
@@ -198,39 +209,42 @@ __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], const u32x4* tb, u
     for (int u = 0; u < U; u++) {
         uint32_t k = lp.k + lane;
         if (k >= cpp) k -= cpp;
-        const uint32_t c = r0 + u * 64 + lane;
-        v[u] = (c < tchunks && k < nch) ? (NT ? load_stream(tb + c) : load_plain(tb + c)) : u32x4{0u, 0u, 0u, 0u};
+        uint32_t c = r0 + u * 64 + lane;
+        // Lanes on stride padding re-read their packet's last data chunk and
+        // lanes past the task its last chunk (lines other lanes fetch anyway;
+        // flat_reduce_rows zeroes them): unconditional loads let the reduce
+        // wait for one row at a time (vmcnt(N)) instead of all U.
+        if (k >= nch) c -= k - nch + 1;
+        c = min(c, tchunks - 1);
+        v[u] = NT ? load_stream(tb + c) : load_plain(tb + c);
         lp.advance(cpp);
     }
 }
 
-template <int U, bool VERIFY>
+template <int U>
 __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r0, uint32_t tchunks, RowPos& pp,
                                                  uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
-                                                 uint64_t p0, uint32_t& flow, bool implicit_flow, uint32_t n_flows,
-                                                 const uint32_t* pseudo, const uint32_t* flow_of, uint32_t lterm,
-                                                 uint16_t* out, uint8_t* ok, int lane) {
+                                                 uint32_t* res, int lane) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t rs = r0 + u * 64;  // wave-uniform
         if (rs < tchunks) {
             if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
-                flat_finish<VERIFY>(acc, p0 + pp.pkt - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
-                if (implicit_flow && ++flow == n_flows) flow = 0;
+                flat_stash(acc, pp.pkt - 1, res, lane);
                 acc = 0;
             }
             uint32_t k = pp.k + lane;
             if (k >= cpp) k -= cpp;
             u32x4 x = v[u];
-            if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
+            if (k >= nch || rs + lane >= tchunks) x = u32x4{0u, 0u, 0u, 0u};
+            else if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
             const uint64_t val = sum4(x);
             const uint32_t b = cpp - pp.k;  // first lane holding the next packet
             if (b >= 64 || pp.pkt + 1 >= np) {
                 acc += val;
             } else {
                 acc += lane < (int)b ? val : 0ull;
-                flat_finish<VERIFY>(acc, p0 + pp.pkt, flow, pseudo, flow_of, lterm, out, ok, lane);
-                if (implicit_flow && ++flow == n_flows) flow = 0;
+                flat_stash(acc, pp.pkt, res, lane);
                 acc = lane < (int)b ? 0ull : val;
             }
         }
@@ -238,16 +252,20 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
     }
 }
 
+template <int U>
+constexpr int flat_waves_per_simd() { return U >= 16 ? 4 : (U >= 8 ? 5 : 6); }
+
 template <int U, bool PIPE, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
                                               uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    __shared__ uint32_t s_res[4][kFlatMaxRun];
     const int lane = threadIdx.x & 63;
+    uint32_t* res = s_res[threadIdx.x >> 6];
     const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     const uint32_t lterm = len_term(len);
-    const bool implicit_flow = pseudo != nullptr && flow_of == nullptr;
     const uint64_t n_tasks = (n + run - 1) / run;
     const TaskRange tr = xcd_tasks(n_tasks, (kflags & kXcdGroups) != 0);
     for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
@@ -255,7 +273,6 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena,
         const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
         const uint32_t tchunks = np * cpp;
         const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
-        uint32_t flow = implicit_flow ? (uint32_t)((flow_origin + p0) % n_flows) : 0u;
         uint64_t acc = 0;
         RowPos lp{0, 0}, pp{0, 0};
         u32x4 v[U];
@@ -265,19 +282,20 @@ __global__ __launch_bounds__(256) void k_flat(const uint8_t* __restrict__ arena,
                 u32x4 nx[U];
                 const bool more = r0 + 64 * U < tchunks;  // wave-uniform
                 if (more) flat_load_rows<U, NT>(nx, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
-                flat_reduce_rows<U, VERIFY>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, p0, flow, implicit_flow,
-                                            n_flows, pseudo, flow_of, lterm, out, ok, lane);
+                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
                 if (more) {
 #pragma unroll
                     for (int u = 0; u < U; u++) v[u] = nx[u];
                 }
             } else {
-                flat_reduce_rows<U, VERIFY>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, p0, flow, implicit_flow,
-                                            n_flows, pseudo, flow_of, lterm, out, ok, lane);
+                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
                 if (r0 + 64 * U < tchunks) flat_load_rows<U, NT>(v, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
             }
         }
-        flat_finish<VERIFY>(acc, p0 + np - 1, flow, pseudo, flow_of, lterm, out, ok, lane);
+        flat_stash(acc, np - 1, res, lane);
+        wave_sync();
+        flat_write<VERIFY>(res, p0, np, pseudo, n_flows, flow_of, flow_origin, lterm, out, ok, lane);
+        wave_sync();
     }
 }
 
@@ -676,7 +694,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)
         const uint32_t flags = g_tune.flags.load();
         const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 64u;
-        const uint32_t run = std::max<uint32_t>(1u, (64u * rows) / cpp);
+        const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
         hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), 0, as_stream(stream),
