@@ -1,3 +1,13 @@
+#!/usr/bin/env python3
+"""Ragged-kernel row-depth probe on cfg4 (8M and 32M packets), arms interleaved.
+
+    python tools/ragged_probe.py
+
+Arms set pipck_tune(0, loads, 0, flags) directly: loads = rows in flight
+(3/5/9 pipelined), flags bit 4 = no packed-tile addressing.  The loads-only
+numbers in profiles/r01_ragged_probe_loads_only.jsonl came from a temporary
+build whose flags bit 6 compiled the reduce out (removed since).
+"""
 import sys, json, statistics
 sys.path.insert(0, "/root/repo")
 import torch
