@@ -156,10 +156,22 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    return s;
+// Inclusive wave-64 prefix sum on the DPP crossbar (GFX9 DPP: row_shr inside
+// 16-lane rows, then row_bcast:15 / row_bcast:31 across rows) -- no LDS trips.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// Wave total as a scalar: the DPP scan's last lane (six VALU steps and one
+// v_readlane; a __shfl_xor butterfly would be six ds_bpermute round trips).
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
 // A finished packet's folded big-endian sum goes to the wave's LDS slot; the
@@ -168,7 +180,7 @@ __device__ __forceinline__ uint32_t wave_reduce_add(uint32_t s) {
 // one would make the next row's wait drain every load in flight.
 constexpr uint32_t kFlatMaxRun = 128;  // packets per wave task
 __device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint32_t* res, int lane) {
-    const uint32_t s = wave_reduce_add(fold64(acc));
+    const uint32_t s = wave_total(fold64(acc));
     if (lane == 0) res[i] = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
 }
 
@@ -302,18 +314,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
 // ---------------------------------------------------------------------------
 // ragged / chain-segment kernel
 // ---------------------------------------------------------------------------
-// Inclusive wave-64 prefix sum on the DPP crossbar (GFX9 DPP: row_shr inside
-// 16-lane rows, then row_bcast:15 / row_bcast:31 across rows) -- no LDS trips.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
 struct RaggedTileLds {
     uint64_t base[64];  // 16-byte-aligned base address of each segment
     uint32_t pre[65];   // exclusive chunk prefix of the tile's segments; pre[64] = total
@@ -421,12 +421,16 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
             continue;
         }
         ragged_flush(t, lane, racc, rseg);
+        // Segment s's share of the row is inc[tail] - inc[head - 1]: the lane
+        // holding its last chunk in the row adds its inclusive prefix, the lane
+        // holding its first chunk (unless that is lane 0) subtracts its
+        // exclusive one.  Both land in acc[s] mod 2^32, whose final value is
+        // the true (non-wrapping) sum, so no cross-lane fetch is needed.
         const uint32_t inc = wave_incl_scan(val);
         const bool last_chunk = hi <= 16;  // this chunk ends its segment
         const bool tail = active && (lane == 63 || last_chunk);
-        const int head_lane = (int)pre - (int)row;  // lane of the segment's first chunk in this row
-        const uint32_t before = __shfl(inc, max(head_lane, 1) - 1, 64);
-        if (tail) atomicAdd(&t.acc[s], inc - (head_lane > 0 ? before : 0u));
+        const bool head = active && rel == 0 && lane > 0;
+        if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
     }
 }
 

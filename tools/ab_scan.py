@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Same-process A/B of two libpipck builds (box-to-box variation is a few %,
+"""Same-process A/B of libpipck builds (box-to-box variation is a few %,
 larger than most kernel changes).
 
-    python tools/ab_scan.py pip_amd/lib/ab/libpipck_base.so
+    python tools/ab_scan.py [--only cfg2,cfg4] pip_amd/lib/ab/libpipck_base.so [more.so ...]
 
-Arm "base" = the given library, arm "cur" = pip_amd/lib/libpipck.so; both run
-the same device batches (generated once), rounds interleaved, results checked
-equal.  One JSON line per (workload, arm).
+Each given library is an arm named after its file stem (minus "libpipck_"),
+arm "cur" = pip_amd/lib/libpipck.so; all run the same device batches
+(generated once), rounds interleaved, results checked equal.  One JSON line
+per (workload, arm).
 """
 from __future__ import annotations
 
@@ -35,9 +36,16 @@ def bind(lib):
 
 def main():
     engine.require_gpu()
-    libs = {"base": bind(C.CDLL(str(Path(sys.argv[1]).resolve()))), "cur": bind(_lib.load())}
+    args = sys.argv[1:]
+    only = None
+    if args and args[0] == "--only":
+        only, args = set(args[1].split(",")), args[2:]
+    libs = {Path(a).stem.replace("libpipck_", ""): bind(C.CDLL(str(Path(a).resolve()))) for a in args}
+    libs["cur"] = bind(_lib.load())
     p = engine._ptr
     for w, n in ((CFG2, 4 << 20), (CFG3, 1 << 20), (CFG5, 8 << 20), (CFG4, 8 << 20)):
+        if only and f"cfg{w.cfg}" not in only:
+            continue
         pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         st = engine.current_stream()

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Kernel throughput vs batch size, with and without the XCD-grouped task split.
+"""Kernel throughput vs batch size for launch-shape arms (engine.tune kwargs).
 
-    python tools/size_scan.py [--iters 10]
+    python tools/size_scan.py [--iters 10] [--only cfg4] [--sizes 8,32] [--arms '{"a": {...}}']
 
-One JSON line per (workload, packets, xcd_groups): median kernel ms (HIP
-events) and algorithmic GB/s.  Both arms run in one process, interleaved.
+One JSON line per (workload, packets, arm): median kernel ms (HIP events) and
+algorithmic GB/s.  All arms run in one process, interleaved, results checked equal.
 """
 from __future__ import annotations
 
@@ -19,7 +19,10 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 import torch  # noqa: E402
 
 from pip_amd import engine  # noqa: E402
-from pip_amd.workloads import CFG4, CFG5, N_FLOWS  # noqa: E402
+from pip_amd.workloads import BY_CFG, CFG4, CFG5, N_FLOWS  # noqa: E402
+
+DEFAULT_SIZES = {1: (1 << 20,), 2: (4 << 20,), 3: (1 << 20,), 4: (8 << 20, 32 << 20),
+                 5: (2 << 20, 4 << 20, 8 << 20, 16 << 20)}
 
 
 def timed(fn, iters):
@@ -39,9 +42,18 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="", help="comma list of cfgN (default cfg5,cfg4)")
+    ap.add_argument("--sizes", default="", help="comma list of packet counts in Mi (default per workload)")
+    ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs} (default: built-in arms)")
     a = ap.parse_args()
     engine.require_gpu()
-    for w, sizes in ((CFG5, (2 << 20, 4 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))):
+    plan = [(CFG5, (2 << 20, 4 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))]
+    if a.only:
+        cfgs = [int(c.strip().lstrip("cfg")) for c in a.only.split(",")]
+        plan = [(BY_CFG[c], DEFAULT_SIZES[c]) for c in cfgs]
+    if a.sizes:
+        plan = [(w, tuple(int(float(x) * (1 << 20)) for x in a.sizes.split(","))) for w, _ in plan]
+    for w, sizes in plan:
         pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
         for n in sizes:
             if w.ragged:
@@ -59,6 +71,8 @@ def main():
             if w.ragged:
                 arms = {"default": {}, "wide_blocks": {"wide_blocks": True}, "loads_8": {"loads_per_lane": 8},
                         "pipe_4": {"loads_per_lane": 5}, "loads_2": {"loads_per_lane": 2}}
+            if a.arms:
+                arms = json.loads(a.arms)
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
