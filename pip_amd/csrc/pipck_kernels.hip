@@ -691,8 +691,9 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        // rows in flight per wave: 16 for jumbo packets, 8 below 4 KiB (measured, profiles/README.md)
-        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (cpp >= 256 ? 16u : 8u);
+        // rows in flight per wave: 16 (cfg2: 0-5 % over 8 in same-process scans,
+        // profiles/r01_size_scan12_cfg2_cfg3.jsonl, r01_flat_taper_scan.jsonl)
+        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : 16u;
         const FlatVariant* fv = &flat_variant(loads);
         // a wave task covers ~64 rows of 1 KiB and the grid holds one task per wave
         // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)

@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma list of cfgN (default cfg5,cfg4)")
     ap.add_argument("--sizes", default="", help="comma list of packet counts in Mi (default per workload)")
-    ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs} (default: built-in arms)")
+    ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs}, or @file (default: built-in arms)")
     a = ap.parse_args()
     engine.require_gpu()
     plan = [(CFG5, (2 << 20, 4 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))]
@@ -72,7 +72,7 @@ def main():
                 arms = {"default": {}, "wide_blocks": {"wide_blocks": True}, "loads_8": {"loads_per_lane": 8},
                         "pipe_4": {"loads_per_lane": 5}, "loads_2": {"loads_per_lane": 2}}
             if a.arms:
-                arms = json.loads(a.arms)
+                arms = json.loads(Path(a.arms[1:]).read_text() if a.arms.startswith("@") else a.arms)
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
