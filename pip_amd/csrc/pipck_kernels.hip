@@ -214,22 +214,50 @@ struct RowPos {
     }
 };
 
+template <bool NT>
+__device__ __forceinline__ void flat_load_row(u32x4& v, const u32x4* tb, uint32_t r, uint32_t tchunks, RowPos& lp,
+                                              uint32_t cpp, uint32_t nch, int lane) {
+    uint32_t k = lp.k + lane;
+    if (k >= cpp) k -= cpp;
+    uint32_t c = r + lane;
+    // Lanes on stride padding re-read their packet's last data chunk and
+    // lanes past the task its last chunk (lines other lanes fetch anyway;
+    // flat_reduce_row zeroes them): unconditional loads let the reduce
+    // wait for one row at a time (vmcnt(N)) instead of all U.
+    if (k >= nch) c -= k - nch + 1;
+    c = min(c, tchunks - 1);
+    v = NT ? load_stream(tb + c) : load_plain(tb + c);
+    lp.advance(cpp);
+}
+
 template <int U, bool NT>
 __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], const u32x4* tb, uint32_t r0, uint32_t tchunks,
                                                RowPos& lp, uint32_t cpp, uint32_t nch, int lane) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        uint32_t k = lp.k + lane;
-        if (k >= cpp) k -= cpp;
-        uint32_t c = r0 + u * 64 + lane;
-        // Lanes on stride padding re-read their packet's last data chunk and
-        // lanes past the task its last chunk (lines other lanes fetch anyway;
-        // flat_reduce_rows zeroes them): unconditional loads let the reduce
-        // wait for one row at a time (vmcnt(N)) instead of all U.
-        if (k >= nch) c -= k - nch + 1;
-        c = min(c, tchunks - 1);
-        v[u] = NT ? load_stream(tb + c) : load_plain(tb + c);
-        lp.advance(cpp);
+    for (int u = 0; u < U; u++) flat_load_row<NT>(v[u], tb, r0 + u * 64, tchunks, lp, cpp, nch, lane);
+}
+
+// rs < tchunks (wave-uniform)
+__device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
+                                                uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
+                                                uint32_t* res, int lane) {
+    if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
+        flat_stash(acc, pp.pkt - 1, res, lane);
+        acc = 0;
+    }
+    uint32_t k = pp.k + lane;
+    if (k >= cpp) k -= cpp;
+    u32x4 x = v;
+    if (k >= nch || rs + lane >= tchunks) x = u32x4{0u, 0u, 0u, 0u};
+    else if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
+    const uint64_t val = sum4(x);
+    const uint32_t b = cpp - pp.k;  // first lane holding the next packet
+    if (b >= 64 || pp.pkt + 1 >= np) {
+        acc += val;
+    } else {
+        acc += lane < (int)b ? val : 0ull;
+        flat_stash(acc, pp.pkt, res, lane);
+        acc = lane < (int)b ? 0ull : val;
     }
 }
 
@@ -240,26 +268,7 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t rs = r0 + u * 64;  // wave-uniform
-        if (rs < tchunks) {
-            if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
-                flat_stash(acc, pp.pkt - 1, res, lane);
-                acc = 0;
-            }
-            uint32_t k = pp.k + lane;
-            if (k >= cpp) k -= cpp;
-            u32x4 x = v[u];
-            if (k >= nch || rs + lane >= tchunks) x = u32x4{0u, 0u, 0u, 0u};
-            else if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
-            const uint64_t val = sum4(x);
-            const uint32_t b = cpp - pp.k;  // first lane holding the next packet
-            if (b >= 64 || pp.pkt + 1 >= np) {
-                acc += val;
-            } else {
-                acc += lane < (int)b ? val : 0ull;
-                flat_stash(acc, pp.pkt, res, lane);
-                acc = lane < (int)b ? 0ull : val;
-            }
-        }
+        if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
         pp.advance(cpp);
     }
 }
@@ -290,14 +299,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
         u32x4 v[U];
         flat_load_rows<U, NT>(v, tb, 0, tchunks, lp, cpp, nch, lane);
         for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
-            if (PIPE) {
-                u32x4 nx[U];
-                const bool more = r0 + 64 * U < tchunks;  // wave-uniform
-                if (more) flat_load_rows<U, NT>(nx, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
-                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
-                if (more) {
+            if (PIPE) {  // ring: a reduced row's registers take the load U rows ahead at once
 #pragma unroll
-                    for (int u = 0; u < U; u++) v[u] = nx[u];
+                for (int u = 0; u < U; u++) {
+                    const uint32_t rs = r0 + u * 64;  // wave-uniform
+                    if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
+                    pp.advance(cpp);
+                    flat_load_row<NT>(v[u], tb, rs + 64 * U, tchunks, lp, cpp, nch, lane);  // unconditional (clamped)
                 }
             } else {
                 flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
@@ -346,32 +354,37 @@ __device__ __forceinline__ uint32_t ragged_seg_of(const RaggedTileLds& t, uint32
     return s;
 }
 
-// Issue the 16-byte loads of U rows of the tile's chunk stream.  A packed tile
-// (segments back to back at 16-byte granularity, see k_ragged) addresses chunk
-// c directly at tbase + 16c, so its loads wait on nothing; otherwise each
-// lane's segment is looked up first to find its base.
+// Issue the 16-byte load of one row (chunks c0 .. c0+63) of the tile's chunk
+// stream.  A packed tile (segments back to back at 16-byte granularity, see
+// k_ragged) addresses chunk c directly at tbase + 16c, so its loads wait on
+// nothing; otherwise each lane's segment is looked up first to find its base.
+template <bool NT>
+__device__ __forceinline__ void ragged_issue_row(const RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
+                                                 u32x4& v, uint32_t& sx, uint32_t& scur, bool packed,
+                                                 uintptr_t tbase) {
+    // Lanes past the tile's last chunk re-read that chunk (same cache line
+    // as a live lane; ragged_reduce ignores them): the loads stay
+    // unconditional, so the reduce can wait for each row alone (vmcnt(N))
+    // instead of draining the whole batch at a branch join.
+    const uint32_t c = min(c0 + lane, total - 1);
+    const u32x4* p;
+    if (packed) {
+        p = reinterpret_cast<const u32x4*>(tbase) + c;
+    } else {
+        const uint32_t s = ragged_seg_of(t, c, scur);
+        sx = s;
+        p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
+    }
+    v = NT ? load_stream(p) : load_plain(p);
+    __builtin_amdgcn_sched_barrier(0);  // keep row order (see flat_load_rows)
+}
+
 template <int U, bool NT>
 __device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
                                              u32x4 (&v)[U], uint32_t (&sx)[U], uint32_t& scur, bool packed,
                                              uintptr_t tbase) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        // Lanes past the tile's last chunk re-read that chunk (same cache line
-        // as a live lane; ragged_reduce ignores them): the loads stay
-        // unconditional, so the reduce can wait for each row alone (vmcnt(N))
-        // instead of draining the whole batch at a branch join.
-        const uint32_t c = min(c0 + u * 64 + lane, total - 1);
-        const u32x4* p;
-        if (packed) {
-            p = reinterpret_cast<const u32x4*>(tbase) + c;
-        } else {
-            const uint32_t s = ragged_seg_of(t, c, scur);
-            sx[u] = s;
-            p = reinterpret_cast<const u32x4*>(t.base[s]) + (c - t.pre[s]);
-        }
-        v[u] = NT ? load_stream(p) : load_plain(p);
-        __builtin_amdgcn_sched_barrier(0);  // keep row order (see flat_load_rows)
-    }
+    for (int u = 0; u < U; u++) ragged_issue_row<NT>(t, c0 + u * 64, total, lane, v[u], sx[u], scur, packed, tbase);
 }
 
 // Add a run of whole rows of one segment (per-lane partials in racc) to the
@@ -384,11 +397,50 @@ __device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_
     rseg = kNoSeg;
 }
 
-// Reduce U rows by segment.  A row lying wholly inside one segment (most rows
+// Reduce one row by segment.  A row lying wholly inside one segment (most rows
 // of multi-KiB packets) only adds into the per-lane run partial racc.  Any
 // other row takes a wave prefix scan: the lane holding a segment's last chunk
 // in the row adds (its prefix - the prefix just before the segment's first
-// chunk in the row) to the segment's LDS partial.
+// chunk in the row) to the segment's LDS partial.  row < total (wave-uniform).
+__device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
+                                                  const u32x4& v, uint32_t sx, uint32_t& racc, uint32_t& rseg,
+                                                  bool packed, uint32_t& scur) {
+    const uint32_t c = row + lane;
+    const bool active = c < total;
+    const uint32_t s = packed ? ragged_seg_of(t, c, scur) : sx;
+    const uint32_t pre = t.pre[s];
+    const uint32_t span = t.span[s];
+    const int rel = (int)(c - pre);
+    const int lo = rel == 0 ? (int)(span & 15) : 0;
+    const int hi = (int)(span >> 4) - 16 * rel;
+    u32x4 x = v;
+    if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
+    else if (hi < 16) x = mask_tail(x, hi);
+    const uint32_t val = active ? fold64(sum4(x)) : 0u;
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+    const uint32_t end0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.pre[s0 + 1]);
+    rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
+    if (end0 >= row + 64) {  // the whole row is in segment s0 (pre[64] = total); wave-uniform
+        if (s0 != rseg) {
+            ragged_flush(t, lane, racc, rseg);
+            rseg = s0;
+        }
+        racc += val;
+        return;
+    }
+    ragged_flush(t, lane, racc, rseg);
+    // Segment s's share of the row is inc[tail] - inc[head - 1]: the lane
+    // holding its last chunk in the row adds its inclusive prefix, the lane
+    // holding its first chunk (unless that is lane 0) subtracts its
+    // exclusive one.  Both land in acc[s] mod 2^32, whose final value is
+    // the true (non-wrapping) sum, so no cross-lane fetch is needed.
+    const uint32_t inc = wave_incl_scan(val);
+    const bool last_chunk = hi <= 16;  // this chunk ends its segment
+    const bool tail = active && (lane == 63 || last_chunk);
+    const bool head = active && rel == 0 && lane > 0;
+    if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
+}
+
 template <int U>
 __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
                                               const u32x4 (&v)[U], const uint32_t (&sx)[U], uint32_t& racc,
@@ -396,69 +448,35 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t row = c0 + u * 64;
-        if (row >= total) continue;  // wave-uniform
-        const uint32_t c = row + lane;
-        const bool active = c < total;
-        const uint32_t s = packed ? ragged_seg_of(t, c, scur) : sx[u];
-        const uint32_t pre = t.pre[s];
-        const uint32_t span = t.span[s];
-        const int rel = (int)(c - pre);
-        const int lo = rel == 0 ? (int)(span & 15) : 0;
-        const int hi = (int)(span >> 4) - 16 * rel;
-        u32x4 x = v[u];
-        if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
-        else if (hi < 16) x = mask_tail(x, hi);
-        const uint32_t val = active ? fold64(sum4(x)) : 0u;
-        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
-        const uint32_t end0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.pre[s0 + 1]);
-        rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
-        if (end0 >= row + 64) {  // the whole row is in segment s0 (pre[64] = total); wave-uniform
-            if (s0 != rseg) {
-                ragged_flush(t, lane, racc, rseg);
-                rseg = s0;
-            }
-            racc += val;
-            continue;
-        }
-        ragged_flush(t, lane, racc, rseg);
-        // Segment s's share of the row is inc[tail] - inc[head - 1]: the lane
-        // holding its last chunk in the row adds its inclusive prefix, the lane
-        // holding its first chunk (unless that is lane 0) subtracts its
-        // exclusive one.  Both land in acc[s] mod 2^32, whose final value is
-        // the true (non-wrapping) sum, so no cross-lane fetch is needed.
-        const uint32_t inc = wave_incl_scan(val);
-        const bool last_chunk = hi <= 16;  // this chunk ends its segment
-        const bool tail = active && (lane == 63 || last_chunk);
-        const bool head = active && rel == 0 && lane > 0;
-        if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
+        if (row < total) ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, packed, scur);  // wave-uniform
     }
 }
 
 // Stream a tile's chunks U rows at a time and reduce them by segment.
+// PIPE = a ring: as soon as row r is reduced, its registers take the load of
+// row r + U, so U rows stay in flight throughout (the plain loop lets the
+// queue run dry while it reduces a batch) at no extra VGPRs.
 template <int U, bool PIPE, bool NT, bool PACKED>
 __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, int lane, uintptr_t tbase,
                                               uint32_t& racc, uint32_t& rseg) {
     u32x4 v[U];
     uint32_t sx[U];
     uint32_t scur = 0, rcur = 0;
-    if (total) ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur, PACKED, tbase);
+    if (!total) return;
+    ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur, PACKED, tbase);
     for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
-        const bool more = c0 + 64 * U < total;  // wave-uniform
         if (PIPE) {
-            u32x4 nv[U];
-            uint32_t nsx[U];
-            if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, nv, nsx, scur, PACKED, tbase);
-            ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, PACKED, rcur);
-            if (more) {
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    v[u] = nv[u];
-                    sx[u] = nsx[u];
-                }
+            for (int u = 0; u < U; u++) {
+                const uint32_t row = c0 + u * 64;
+                if (row < total) ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, PACKED, rcur);
+                // unconditional (clamped) reload: the VM count stays static, so each
+                // reduce waits for its own row only (vmcnt(U-1))
+                ragged_issue_row<NT>(t, row + 64 * U, total, lane, v[u], sx[u], scur, PACKED, tbase);
             }
         } else {
             ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, PACKED, rcur);
-            if (more) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
+            if (c0 + 64 * U < total) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
         }
     }
 }
@@ -628,7 +646,8 @@ struct FlatVariant {
     }
 // loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9 = pipelined U = 2/4/8
 static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_F(8, false), PIPCK_F(16, false),
-                                    PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true)};
+                                    PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
+                                    PIPCK_F(16, true)};
 #undef PIPCK_F
 static const FlatVariant& flat_variant(uint32_t loads) {
     switch (loads) {
@@ -639,6 +658,8 @@ static const FlatVariant& flat_variant(uint32_t loads) {
         case 5: return kFlat[5];
         case 9: return kFlat[6];
         case 16: return kFlat[3];
+        case 13: return kFlat[7];
+        case 17: return kFlat[8];
         default: return kFlat[2];
     }
 }
@@ -691,9 +712,10 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        // rows in flight per wave: 16 (cfg2: 0-5 % over 8 in same-process scans,
-        // profiles/r01_size_scan12_cfg2_cfg3.jsonl, r01_flat_taper_scan.jsonl)
-        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : 16u;
+        // rows in flight per wave: a ring of 16 (cfg2: 0-5 % over 8 plain rows,
+        // profiles/r01_size_scan12_cfg2_cfg3.jsonl; ring vs plain 16: cfg2 +1 %,
+        // cfg3 +0.5 %, cfg5 even, profiles/r01_flat_ring_scan.jsonl)
+        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : 17u;
         const FlatVariant* fv = &flat_variant(loads);
         // a wave task covers ~64 rows of 1 KiB and the grid holds one task per wave
         // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)
@@ -753,8 +775,9 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
     // loads_per_lane: 2/4/8/16 rows in flight on packed tiles (at most 4 on
-    // others), 3/5/9 = pipelined 2/4/8 (default: 4)
-    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 4u;
+    // others), 3/5/7/9/13/17 = ring-pipelined 2/4/6/8/12/16.  Default: ring of
+    // 12 (cfg4 +2.5 % over plain 4, profiles/r01_ragged_ring_scan.jsonl)
+    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 13u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {
@@ -764,6 +787,9 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
         case 16: launch_ragged_u<16, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         case 3: launch_ragged_u<2, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         case 9: launch_ragged_u<8, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 7: launch_ragged_u<6, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 13: launch_ragged_u<12, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 17: launch_ragged_u<16, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         default: launch_ragged_u<4, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
     }
     PIPCK_LAUNCHED("k_ragged");

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Ragged kernel vs packet-length distribution, next to the fixed-stride path
+on the same arena where one exists (uniform lengths give a packed arena whose
+stride is roundup16(len), i.e. the fixed layout).
+
+    python tools/ragged_shapes.py [--iters 10]
+
+One JSON line per (shape, path): median kernel ms (HIP events), algorithmic GB/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+import torch  # noqa: E402
+
+from pip_amd import engine  # noqa: E402
+from pip_amd.workloads import CFG4, N_FLOWS  # noqa: E402
+from size_scan import timed  # noqa: E402
+
+SHAPES = [("uniform_8980", 8980, 2 << 20), ("uniform_1480", 1480, 8 << 20), ("uniform_512", 512, 16 << 20),
+          ("uniform_128", 128, 32 << 20), ("zipf_cfg4", 0, 8 << 20), ("zipf_cfg4_32M", 0, 32 << 20)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    engine.require_gpu()
+    w = CFG4
+    pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
+    for name, length, n in SHAPES:
+        if a.only and name not in a.only.split(","):
+            continue
+        lengths = None if length == 0 else torch.full((n,), length, dtype=torch.int32, device="cuda")
+        arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS, lengths=lengths)
+        nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
+        arms = {"ragged": lambda: engine.checksum_ragged(arena, desc, pseudo)}
+        if length:
+            stride = (length + 15) // 16 * 16
+            arms["fixed"] = lambda: engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS)
+        res, ref = {}, None
+        for _ in range(5):
+            for k, fn in arms.items():
+                res.setdefault(k, []).append(timed(fn, a.iters))
+                out = fn()
+                if ref is None:
+                    ref = out.clone()
+                elif k == "fixed":
+                    # fixed-path flows are (origin + i) % n_flows, the same as gen_ragged's descriptors
+                    assert torch.equal(out, ref), name
+        for k, ms in res.items():
+            m = statistics.median(ms)
+            print(json.dumps({"shape": name, "packets": n, "gbytes": round(nbytes / 1e9, 2), "path": k,
+                              "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}), flush=True)
+        del arena, desc, lens
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
