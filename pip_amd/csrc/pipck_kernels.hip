@@ -327,6 +327,7 @@ struct RaggedTileLds {
     uint32_t pre[65];   // exclusive chunk prefix of the tile's segments; pre[64] = total
     uint32_t acc[64];   // LE residue partial per segment
     uint32_t span[64];  // (end << 4) | head, relative to the 16-byte-aligned base
+    uint32_t mark[64];  // packed tiles: (row tag << 6) | segment starting at chunk row + i (max wins)
 };
 
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
@@ -389,9 +390,9 @@ __device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0
 
 // Add a run of whole rows of one segment (per-lane partials in racc) to the
 // segment's LDS partial: one wave sum, one LDS add.
-__device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_t& racc, uint32_t& rseg) {
+__device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint64_t& racc, uint32_t& rseg) {
     if (rseg == kNoSeg) return;  // wave-uniform
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(racc), 63);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(fold64(racc)), 63);
     if (lane == 0) atomicAdd(&t.acc[rseg], tot);
     racc = 0;
     rseg = kNoSeg;
@@ -403,7 +404,7 @@ __device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_
 // in the row adds (its prefix - the prefix just before the segment's first
 // chunk in the row) to the segment's LDS partial.  row < total (wave-uniform).
 __device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
-                                                  const u32x4& v, uint32_t sx, uint32_t& racc, uint32_t& rseg,
+                                                  const u32x4& v, uint32_t sx, uint64_t& racc, uint32_t& rseg,
                                                   bool packed, uint32_t& scur) {
     const uint32_t c = row + lane;
     const bool active = c < total;
@@ -441,9 +442,69 @@ __device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row
     if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
 }
 
+// Inclusive wave-64 max-scan (same DPP pattern as wave_incl_scan).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
+}
+
+// Reduce one row of a packed tile.  Lane i of the wave holds segment i's
+// chunk range [pre_v, end_v) in registers, so the segment s0 of the row's
+// first chunk is a ballot popcount (pre is non-decreasing: the segments
+// starting at or before chunk c are a prefix), kept as scalars across rows.
+// A row strictly inside s0 (e0 > row + 64: no segment end, and packed
+// segments have no head bytes) needs no per-lane lookup or mask at all: its
+// chunks just add into the u64 run partial.  A mixed row finds every lane's
+// segment without a search: each segment starting inside the row marks its
+// first chunk's slot (LDS max, tagged by row so stale marks lose), and a wave
+// max-scan seeded with s0 carries the last start to every later lane.
+__device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
+                                                         const u32x4& v, uint32_t pre_v, uint32_t end_v,
+                                                         uint32_t& s0, uint32_t& e0, uint64_t& racc,
+                                                         uint32_t& rseg) {
+    if (row >= e0) {  // wave-uniform: the row starts past segment s0
+        s0 = (uint32_t)__popcll(__ballot(pre_v <= row)) - 1u;
+        e0 = (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)s0);
+    }
+    s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
+    e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e0);
+    rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
+    if (e0 > row + 64) {  // interior row: all 64 chunks are whole chunks of s0 (and < total)
+        if (s0 != rseg) {
+            ragged_flush(t, lane, racc, rseg);
+            rseg = s0;
+        }
+        racc += sum4(v);
+        return;
+    }
+    ragged_flush(t, lane, racc, rseg);
+    const uint32_t tag = ((row >> 6) + 1u) << 6;
+    if (pre_v > row && pre_v < row + 64) atomicMax(&t.mark[pre_v - row], tag | (uint32_t)lane);
+    wave_sync();
+    const uint32_t m = t.mark[lane];
+    const uint32_t s = wave_incl_max(lane == 0 ? s0 : (m >= tag ? (m & 63u) : 0u));
+    const uint32_t c = row + lane;
+    const bool active = c < total;
+    const int rel = (int)(c - t.pre[s]);
+    const int hi = (int)(t.span[s] >> 4) - 16 * rel;  // packed: no head bytes
+    u32x4 x = v;
+    if (hi < 16) x = mask_tail(x, hi);
+    const uint32_t val = active ? fold64(sum4(x)) : 0u;
+    // segment sums by the head/tail prefix trick (see ragged_reduce_row)
+    const uint32_t inc = wave_incl_scan(val);
+    const bool tail = active && (lane == 63 || hi <= 16);
+    const bool head = active && rel == 0 && lane > 0;
+    if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
+}
+
 template <int U>
 __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
-                                              const u32x4 (&v)[U], const uint32_t (&sx)[U], uint32_t& racc,
+                                              const u32x4 (&v)[U], const uint32_t (&sx)[U], uint64_t& racc,
                                               uint32_t& rseg, bool packed, uint32_t& scur) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -458,10 +519,11 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
 // queue run dry while it reduces a batch) at no extra VGPRs.
 template <int U, bool PIPE, bool NT, bool PACKED>
 __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, int lane, uintptr_t tbase,
-                                              uint32_t& racc, uint32_t& rseg) {
+                                              uint32_t pre_v, uint32_t end_v, uint64_t& racc, uint32_t& rseg) {
     u32x4 v[U];
     uint32_t sx[U];
     uint32_t scur = 0, rcur = 0;
+    uint32_t s0 = 0, e0 = 0;  // packed: segment of the row's first chunk and its end (scalars)
     if (!total) return;
     ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur, PACKED, tbase);
     for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
@@ -469,13 +531,26 @@ __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, 
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t row = c0 + u * 64;
-                if (row < total) ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, PACKED, rcur);
+                if (row < total) {  // wave-uniform
+                    if (PACKED)
+                        ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, end_v, s0, e0, racc, rseg);
+                    else
+                        ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, false, rcur);
+                }
                 // unconditional (clamped) reload: the VM count stays static, so each
                 // reduce waits for its own row only (vmcnt(U-1))
                 ragged_issue_row<NT>(t, row + 64 * U, total, lane, v[u], sx[u], scur, PACKED, tbase);
             }
         } else {
-            ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, PACKED, rcur);
+            if (PACKED) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t row = c0 + u * 64;
+                    if (row < total) ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, end_v, s0, e0, racc, rseg);
+                }
+            } else {
+                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, false, rcur);
+            }
             if (c0 + 64 * U < total) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
         }
     }
@@ -523,6 +598,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         t.span[lane] = ((head + len) << 4) | head;
         t.base[lane] = addr - head;
         t.acc[lane] = 0;
+        t.mark[lane] = 0;
         // Packed tile: every segment starts 16-byte aligned right where the
         // previous one's chunks end (the layout of pip's TX batches and of the
         // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
@@ -531,11 +607,12 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         const bool packed = (kflags & kNoPackedTiles) == 0 && __all(head == 0 && link);
         const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
         wave_sync();
-        uint32_t racc = 0, rseg = kNoSeg;
+        uint64_t racc = 0;
+        uint32_t rseg = kNoSeg;
         if (packed)
-            ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, racc, rseg);
+            ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
         else  // fewer rows in flight: the lookup path needs a segment register per row
-            ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, racc, rseg);
+            ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
         ragged_flush(t, lane, racc, rseg);
         wave_sync();
         if (valid) {
