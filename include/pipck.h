@@ -148,7 +148,9 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
  * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
  * fixed kernel, bit 3 = XCD-grouped task split, bit 4 = no packed-tile
  * addressing in the ragged kernel, bit 5 = 4-wave ragged blocks (default 1),
- * bits 8.. = 1 KiB rows per flat-kernel wave task (default 64). */
+ * bit 6 = never the small-packet kernel (packets <= 64 B incl. chunk offset),
+ * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bits 16..23
+ * = ragged tiles per wave (default 1). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */

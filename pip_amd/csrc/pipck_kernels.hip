@@ -115,6 +115,81 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
 }
 
 // ---------------------------------------------------------------------------
+// small-packet kernel: one lane per packet, K packets per lane in flight
+// ---------------------------------------------------------------------------
+// For packets of at most 64 bytes including their offset in the first 16-byte
+// chunk (cfg1's 20-byte IPv4 headers at a 24-byte stride).  A wave owns 64*K
+// consecutive packets; lane l takes packets base + 64k + l, so each of the K*NL
+// load instructions reads 64 packets' chunks from one contiguous span.  Every
+// data and flow-table load of the task is issued before the first reduce, and
+// the 2-byte results are stored last (loads and stores share VM_CNT on gfx9):
+// the k_fixed loop instead waits on each packet's loads, then on its flow
+// entry, then stores, so it holds little in flight.  One task per wave (the
+// dispatcher is the queue, as in k_flat).
+template <int NL, int K, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
+                                               uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t base = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64u * K);
+    if (base >= n) return;  // wave-uniform
+    u32x4 v[K][NL];
+    uint32_t P[K];
+    uint32_t flow = 0;
+    if (pseudo && !flow_of) flow = (uint32_t)((flow_origin + base + lane) % n_flows);
+    const uint32_t fstep = pseudo && !flow_of ? 64u % n_flows : 0u;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t pkt = base + 64u * k + lane;
+        const uintptr_t addr = (uintptr_t)arena + pkt * stride;
+        const int head = (int)(addr & 15);
+        const u32x4* b = reinterpret_cast<const u32x4*>(addr - head);
+        const int nch = pkt < n && len ? (head + (int)len + 15) >> 4 : 0;
+#pragma unroll
+        for (int j = 0; j < NL; j++)
+            v[k][j] = j < nch ? (NT ? load_stream(b + j) : load_plain(b + j)) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t pkt = base + 64u * k + lane;
+        P[k] = 0;
+        if (pseudo && pkt < n) P[k] = pseudo[flow_of ? flow_of[pkt] : flow];
+        flow += fstep;
+        if (flow >= n_flows) flow -= n_flows;
+    }
+    const uint32_t lterm = pseudo ? len_term(len) : 0u;
+    uint32_t res[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t pkt = base + 64u * k + lane;
+        const uintptr_t addr = (uintptr_t)arena + pkt * stride;
+        const int head = (int)(addr & 15);
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < NL; j++) {
+            const int lo = j == 0 ? head : 0;
+            const int hi = head + (int)len - 16 * j;
+            u32x4 x = v[k][j];
+            if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+            acc += sum4(x);
+        }
+        const uint32_t F = be_fold(fold64(acc), addr);
+        res[k] = VERIFY ? (uint32_t)(fold16(P[k] + lterm + F) == 0xFFFFu) : (uint32_t)finish(P[k] + lterm, F);
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint64_t pkt = base + 64u * k + lane;
+        if (pkt < n) {
+            if (VERIFY)
+                ok[pkt] = (uint8_t)res[k];
+            else
+                out[pkt] = (uint16_t)res[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // task split shared by the streaming kernels
 // ---------------------------------------------------------------------------
 // Static grid-stride over tasks; with the default grid (one task per wave,
@@ -705,6 +780,29 @@ static const Variant& pick_variant(uint32_t nch) {
     return best ? *best : kVariants[kNumVariants - 1];
 }
 
+constexpr uint32_t kNoSmall = 64u;  // pipck_tune flags bit 6: never the small-packet kernel
+struct SmallVariant {
+    int k;              // packets per lane per wave task
+    fixed_fn fn[4][2][2];  // [nl-1][verify][nt]
+};
+#define PIPCK_S1(NL, K)                                                                            \
+    {                                                                                              \
+        {k_small<NL, K, false, false>, k_small<NL, K, false, true>},                               \
+            {k_small<NL, K, true, false>, k_small<NL, K, true, true>}                              \
+    }
+#define PIPCK_S(K) {K, {PIPCK_S1(1, K), PIPCK_S1(2, K), PIPCK_S1(3, K), PIPCK_S1(4, K)}}
+// tune flags bits 24..27 select K (1 = 2, 2 = 4, 3 = 8, 4 = 16); default 2:
+// deeper tasks measured slower (cfg1 at 64M-256M headers: K = 2 / 4 / 8 / 16
+// -> 4.19 / 4.15 / 3.83 / 3.87 TB/s, plain loads beat nt by 10 %,
+// profiles/r01_small_kernel_scan.jsonl)
+static const SmallVariant kSmall[] = {PIPCK_S(2), PIPCK_S(4), PIPCK_S(8), PIPCK_S(16)};
+#undef PIPCK_S
+#undef PIPCK_S1
+static const SmallVariant& small_variant() {
+    const uint32_t k = (g_tune.flags.load() >> 24) & 0xFu;
+    return kSmall[k >= 1 && k <= 4 ? k - 1 : 0];
+}
+
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
@@ -805,6 +903,21 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");
+        return PIPCK_OK;
+    }
+    // Largest in-chunk offset any packet start can have: starts are
+    // arena + i*stride, so their offsets mod 16 step by g = gcd(stride, 16).
+    uint32_t g = 16;
+    while (g > 1 && stride % g) g >>= 1;
+    const uint32_t hmax = (uint32_t)((uintptr_t)d_arena % g) + 16u - g;
+    const uint32_t small_nl = (hmax + len + 15u) / 16u;
+    if (!g_tune.lanes.load() && !(g_tune.flags.load() & kNoSmall) && small_nl <= 4) {
+        const SmallVariant& sv = small_variant();
+        const uint64_t waves = (n + 64u * sv.k - 1) / (64u * sv.k);
+        hipLaunchKernelGGL(sv.fn[small_nl ? small_nl - 1 : 0][verify][nt_for(false)], dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0,
+                           as_stream(stream), (const uint8_t*)d_arena, stride, len, n, d_pseudo,
+                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
+        PIPCK_LAUNCHED("k_small");
         return PIPCK_OK;
     }
     const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;

@@ -216,6 +216,50 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
         engine.tune()
 
 
+@pytest.mark.parametrize("misalign", [0, 1, 4, 8, 13])
+def test_small_packet_kernel_vs_oracle(oracle, misalign):
+    """k_small (one lane per packet, <= 64 bytes incl. the first chunk's offset):
+    every length 0..49 at tight, odd, 8- and 16-aligned strides (and strides
+    below 16), partial last tasks, implicit and explicit flows, RX verify; the
+    same batches through k_fixed (small=False) must agree."""
+    rng = np.random.default_rng(500 + misalign)
+    try:
+        for length in range(0, 50):
+            for stride in sorted({max(length, 1), length + 1, length + 3, (length + 7) // 8 * 8 or 8,
+                                  (length + 15) // 16 * 16 or 16, 24 if length <= 24 else length}):
+                n = int(rng.choice([1, 255, 256, 257, 1000, 1500]))
+                fam = int(rng.choice([0, 4, 6]))
+                host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
+                if n > 3:
+                    host[stride:2 * stride] = 0xFF
+                    host[2 * stride:3 * stride] = 0
+                _, arena = upload(host, misalign)
+                seed, proto, origin = int(rng.integers(0, 2**62)), 17, int(rng.integers(0, 3000))
+                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+                engine.tune()
+                got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                assert np.array_equal(got, want), (length, stride, n, fam, np.nonzero(got != want)[0][:5])
+                ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
+                assert np.array_equal(ok.astype(bool), got == 0)
+                engine.tune(small=False)
+                old = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                assert np.array_equal(old, want)
+        # explicit per-packet flow indices
+        n, L = 3001, 20
+        host = rng.integers(0, 256, n * 24, dtype=np.uint8)
+        _, arena = upload(host, misalign)
+        _, pseudo = engine.gen_flows(4, N_FLOWS, 99, 6)
+        flow_of = rng.integers(0, N_FLOWS, n).astype(np.int32)
+        engine.tune()
+        got = u16(engine.checksum_fixed(arena, 24, L, n, pseudo, N_FLOWS, torch.from_numpy(flow_of).to(DEV), 0))
+        for i in range(0, n, 7):
+            s, d = oracle.flow4(99, int(flow_of[i]))
+            assert got[i] == oracle.inet_checksum(host[i * 24:i * 24 + L].tobytes(), 6, s, d)
+    finally:
+        engine.tune()
+
+
 def test_fixed_grid_stride_loop(oracle):
     """Force a tiny grid so every block loops over many packets."""
     rng = np.random.default_rng(5)

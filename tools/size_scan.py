@@ -78,7 +78,7 @@ def main():
                     engine.tune(**kw)
                     res.setdefault(xcd, []).append(timed(run, a.iters))
                     out = run()
-                    if xcd == "default":
+                    if rnd == 0 and xcd == next(iter(arms)):
                         ref = out.clone()
                     else:
                         assert torch.equal(out, ref)
