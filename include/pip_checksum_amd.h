@@ -52,5 +52,11 @@ void pip_inet6_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto
 void pip_ip_checksum_deferred(const void* hdr, uint32_t len, void* csum_field);
 uint64_t pip_checksum_amd_pending();
 void pip_checksum_amd_flush();
+// Pipelined form of flush (pipck_txq_submit / pipck_txq_complete): submit
+// starts the queued batch on the GPU and returns, so the thread can build the
+// next batch meanwhile; the submitted packets' fields are stored by the next
+// submit, complete or flush on this thread -- output them only after that.
+void pip_checksum_amd_submit();
+void pip_checksum_amd_complete();
 
 #endif

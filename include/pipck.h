@@ -223,9 +223,20 @@ int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t 
                    const uint8_t* dst, void* csum_field);
 /* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);
+/* packets added since the last submit/flush */
 uint64_t pipck_txq_pending(const pipck_txq* q);
 /* Synchronous: returns once every queued field holds its checksum; the queue is then empty. */
 int pipck_txq_flush(pipck_txq* q);
+/* Asynchronous flush, double-buffered: submit starts the queued batch (H2D,
+ * kernels, D2H on the queue's stream) and returns; new adds go to a second
+ * batch meanwhile.  complete waits for the submitted batch and stores its
+ * fields.  At most one batch is in flight: submit first completes the previous
+ * one.  Fields of a submitted batch hold their checksums only after the next
+ * complete, submit or flush returns. */
+int pipck_txq_submit(pipck_txq* q);
+int pipck_txq_complete(pipck_txq* q);
+/* packets submitted and not yet completed */
+uint64_t pipck_txq_inflight(const pipck_txq* q);
 
 #ifdef __cplusplus
 }

@@ -155,10 +155,11 @@ static void tcp_session(const Peer& pe, uint16_t mss, uint32_t write_len) {
 // The deferred (batched) TX API of libpip_checksum_amd.so on real pip_buf
 // chains built by pip's own pip_buf class: every emitted IPv4 header and
 // TCP/UDP segment is rebuilt as a chain (header with its checksum zeroed ->
-// payload split at an odd offset), queued, and flushed in one batch; each
-// stored field must equal the checksum pip put on the wire.  Printed to
-// stderr so stdout stays comparable with pip's own build.
-static void deferred_check() {
+// payload split at an odd offset), queued, and flushed in one batch (or, with
+// `pipelined`, submitted every 5 packets while the next ones are queued, then
+// completed); each stored field must equal the checksum pip put on the wire.
+// Printed to stderr so stdout stays comparable with pip's own build.
+static void deferred_check(bool pipelined) {
     struct Item {
         std::vector<uint8_t> hdr, body;
         uint8_t field[2];
@@ -167,7 +168,9 @@ static void deferred_check() {
     std::vector<Item> items(g_out.size() * 2);
     std::vector<std::shared_ptr<pip_buf>> keep;
     size_t k = 0;
+    size_t npk = 0;
     for (auto& pk : g_out) {
+        if (pipelined && npk++ % 5 == 4) pip_checksum_amd_submit();
         const int ver = pk[0] >> 4;
         const size_t hl = ver == 4 ? 20 : 40;
         const uint8_t proto = ver == 4 ? pk[9] : pk[6];
@@ -215,12 +218,17 @@ static void deferred_check() {
         }
     }
     const unsigned long long pending = pip_checksum_amd_pending();
-    pip_checksum_amd_flush();
+    if (pipelined) {
+        pip_checksum_amd_submit();
+        pip_checksum_amd_complete();
+    } else {
+        pip_checksum_amd_flush();
+    }
     int bad = 0;
     for (size_t i = 0; i < k; i++)
         if ((uint16_t)(items[i].field[0] << 8 | items[i].field[1]) != items[i].wire) bad++;
-    fprintf(stderr, "DEFERRED queued %llu checked %zu bad %d pending_after %llu\n", pending, k, bad,
-            (unsigned long long)pip_checksum_amd_pending());
+    fprintf(stderr, "DEFERRED mode %s queued %llu checked %zu bad %d pending_after %llu\n",
+            pipelined ? "pipelined" : "flush", pending, k, bad, (unsigned long long)pip_checksum_amd_pending());
 }
 #endif
 
@@ -261,7 +269,8 @@ int main() {
     }
     printf("PACKETS %zu VERIFY_BAD %d\n", g_out.size(), bad);
 #ifdef PIPCK_DEFERRED_CHECK
-    deferred_check();
+    deferred_check(false);
+    deferred_check(true);
 #endif
     fflush(stdout);
     _exit(0);  // pip's timer thread is detached and never stops

@@ -165,3 +165,13 @@ void pip_checksum_amd_flush() {
     int rc = pipck_txq_flush(t_ctx.queue());
     if (rc) die("pipck_txq_flush", rc);
 }
+
+void pip_checksum_amd_submit() {
+    int rc = pipck_txq_submit(t_ctx.queue());
+    if (rc) die("pipck_txq_submit", rc);
+}
+
+void pip_checksum_amd_complete() {
+    int rc = pipck_txq_complete(t_ctx.queue());
+    if (rc) die("pipck_txq_complete", rc);
+}

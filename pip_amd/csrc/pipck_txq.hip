@@ -86,14 +86,9 @@ struct DevBuf {
     }
 };
 
-}  // namespace pipck
-
-using namespace pipck;
-
-struct pipck_txq {
-    pipck_ctx* ctx = nullptr;
-    hipStream_t stream = nullptr;
-    int device = 0;
+// One batch of queued packets: host staging, bookkeeping and device buffers.
+// A queue holds two, so one can be filled while the other is in flight.
+struct TxBatch {
     PinnedBuf bytes;                       // segment bytes, each segment 16-byte aligned
     std::vector<pipck_desc> inet_segs;     // offsets into `bytes`
     std::vector<uint64_t> inet_begin{0};   // CSR: packet p owns inet_segs[begin[p], begin[p+1])
@@ -104,17 +99,48 @@ struct pipck_txq {
     PinnedBuf meta;     // staging for descriptors/records and results
     DevBuf d_all;       // device copy of bytes + meta
     DevBuf d_work;      // pseudo bases, scratch, results
+    size_t o_res = 0;   // offset of the results in `meta` (valid while in flight)
+    uint64_t pending() const { return inet_field.size() + ip_field.size(); }
+    void clear() {
+        bytes.size = 0;
+        inet_segs.clear();
+        inet_begin.assign(1, 0);
+        inet_pseudo.clear();
+        inet_field.clear();
+        ip_hdrs.clear();
+        ip_field.clear();
+    }
+    void release() {
+        bytes.release();
+        meta.release();
+        d_all.release();
+        d_work.release();
+    }
+};
+
+}  // namespace pipck
+
+using namespace pipck;
+
+struct pipck_txq {
+    pipck_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // recorded after the in-flight batch's D2H copy
+    int device = 0;
+    TxBatch batch[2];
+    int cur = 0;         // batch receiving adds
+    bool inflight = false;  // batch[cur ^ 1] has been submitted and not completed
 };
 
 namespace {
 
-int append_bytes(pipck_txq* q, const void* src, uint32_t len, uint64_t* off) {
-    const size_t at = (q->bytes.size + 15) & ~(size_t)15;
-    int rc = q->bytes.reserve(at + len);
+int append_bytes(TxBatch* b, const void* src, uint32_t len, uint64_t* off) {
+    const size_t at = (b->bytes.size + 15) & ~(size_t)15;
+    int rc = b->bytes.reserve(at + len);
     if (rc) return rc;
-    if (at > q->bytes.size) std::memset(q->bytes.p + q->bytes.size, 0, at - q->bytes.size);
-    if (len) std::memcpy(q->bytes.p + at, src, len);
-    q->bytes.size = at + len;
+    if (at > b->bytes.size) std::memset(b->bytes.p + b->bytes.size, 0, at - b->bytes.size);
+    if (len) std::memcpy(b->bytes.p + at, src, len);
+    b->bytes.size = at + len;
     *off = at;
     return PIPCK_OK;
 }
@@ -130,16 +156,97 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
             return PIPCK_ERANGE;
         }
     }
+    TxBatch* b = &q->batch[q->cur];
     for (uint32_t i = 0; i < nseg; i++) {
         uint64_t off = 0;
-        int rc = append_bytes(q, segs[i].ptr, segs[i].len, &off);
+        int rc = append_bytes(b, segs[i].ptr, segs[i].len, &off);
         if (rc) return rc;
-        q->inet_segs.push_back(pipck_desc{off, segs[i].len, 0});
+        b->inet_segs.push_back(pipck_desc{off, segs[i].len, 0});
     }
-    q->inet_begin.push_back(q->inet_segs.size());
-    q->inet_pseudo.push_back(ps);
-    q->inet_field.push_back((uint8_t*)field);
+    b->inet_begin.push_back(b->inet_segs.size());
+    b->inet_pseudo.push_back(ps);
+    b->inet_field.push_back((uint8_t*)field);
     return PIPCK_OK;
+}
+
+// Enqueue batch b on the queue's stream: H2D of bytes + metadata, the
+// pseudo-header and chain kernels, ragged IPv4 headers, D2H of the results.
+int enqueue(pipck_txq* q, TxBatch* b) {
+    const uint64_t n_in = b->inet_field.size(), n_ip = b->ip_field.size(), n_seg = b->inet_segs.size();
+    // meta layout (each part 16-byte aligned): inet segs | inet begin | pseudo recs | flow ids | ip descs | results
+    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    const size_t o_segs = 0, o_begin = al(o_segs + n_seg * sizeof(pipck_desc));
+    const size_t o_rec = al(o_begin + (n_in + 1) * sizeof(uint64_t));
+    const size_t o_flow = al(o_rec + n_in * sizeof(TxPseudo));
+    const size_t o_ip = al(o_flow + n_in * sizeof(uint32_t));
+    const size_t o_res = al(o_ip + n_ip * sizeof(pipck_desc));
+    const size_t meta_in = o_res, meta_all = al(o_res + (n_in + n_ip) * sizeof(uint16_t));
+    int rc = b->meta.reserve(meta_all);
+    if (rc) return rc;
+    uint8_t* m = b->meta.p;
+    if (n_seg) std::memcpy(m + o_segs, b->inet_segs.data(), n_seg * sizeof(pipck_desc));
+    std::memcpy(m + o_begin, b->inet_begin.data(), (n_in + 1) * sizeof(uint64_t));
+    if (n_in) std::memcpy(m + o_rec, b->inet_pseudo.data(), n_in * sizeof(TxPseudo));
+    uint32_t* flow = reinterpret_cast<uint32_t*>(m + o_flow);
+    for (uint64_t i = 0; i < n_in; i++) flow[i] = (uint32_t)i;  // packet i uses pseudo base i
+    if (n_ip) std::memcpy(m + o_ip, b->ip_hdrs.data(), n_ip * sizeof(pipck_desc));
+
+    const size_t nb = al(b->bytes.size);
+    if ((rc = b->d_all.reserve(nb + meta_all))) return rc;
+    if ((rc = b->d_work.reserve(al(n_in * 4) + al(std::max<uint64_t>(n_seg, 1) * 4) + 16))) return rc;
+    uint8_t* d_bytes = (uint8_t*)b->d_all.p;
+    uint8_t* d_meta = d_bytes + nb;
+    uint32_t* d_pseudo = (uint32_t*)b->d_work.p;
+    uint32_t* d_scratch = (uint32_t*)((uint8_t*)b->d_work.p + al(n_in * 4));
+    hipStream_t s = q->stream;
+    if (b->bytes.size) PIPCK_HIP(hipMemcpyAsync(d_bytes, b->bytes.p, b->bytes.size, hipMemcpyHostToDevice, s));
+    PIPCK_HIP(hipMemcpyAsync(d_meta, m, meta_in, hipMemcpyHostToDevice, s));
+    uint16_t* d_res = (uint16_t*)(d_meta + o_res);
+    if (n_in) {
+        hipLaunchKernelGGL(k_tx_pseudo, dim3((uint32_t)((n_in + 255) / 256)), dim3(256), 0, s,
+                           (const TxPseudo*)(d_meta + o_rec), (uint32_t)n_in, d_pseudo);
+        PIPCK_LAUNCHED("k_tx_pseudo");
+        rc = pipck_checksum_chains(d_bytes, (const pipck_desc*)(d_meta + o_segs), n_seg,
+                                   (const uint64_t*)(d_meta + o_begin), (const uint32_t*)(d_meta + o_flow), n_in,
+                                   d_pseudo, d_scratch, d_res, nullptr, s);
+        if (rc) return rc;
+    }
+    if (n_ip) {
+        rc = pipck_checksum_ragged(d_bytes, (const pipck_desc*)(d_meta + o_ip), n_ip, nullptr, d_res + n_in, nullptr, s);
+        if (rc) return rc;
+    }
+    PIPCK_HIP(hipMemcpyAsync(m + o_res, d_res, (n_in + n_ip) * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    PIPCK_HIP(hipEventRecord(q->done, s));
+    b->o_res = o_res;
+    return PIPCK_OK;
+}
+
+// Wait for the in-flight batch and store htons(result) into its fields.
+int complete_inflight(pipck_txq* q) {
+    if (!q->inflight) return PIPCK_OK;
+    TxBatch* b = &q->batch[q->cur ^ 1];
+    PIPCK_HIP(hipEventSynchronize(q->done));
+    const uint64_t n_in = b->inet_field.size(), n = b->pending();
+    const uint16_t* res = reinterpret_cast<const uint16_t*>(b->meta.p + b->o_res);
+    for (uint64_t i = 0; i < n; i++) {  // htons(result) into the field (pip_tcp_packet.cpp:132-133)
+        uint8_t* f = i < n_in ? b->inet_field[i] : b->ip_field[i - n_in];
+        f[0] = (uint8_t)(res[i] >> 8);
+        f[1] = (uint8_t)res[i];
+    }
+    b->clear();
+    q->inflight = false;
+    return PIPCK_OK;
+}
+
+// Runs `fn` with the queue's device current, restoring the caller's.
+template <class F>
+int on_device(pipck_txq* q, F fn) {
+    int prev = 0;
+    PIPCK_HIP(hipGetDevice(&prev));
+    if (prev != q->device) PIPCK_HIP(hipSetDevice(q->device));
+    const int rc = fn();
+    if (prev != q->device) PIPCK_HIP(hipSetDevice(prev));
+    return rc;
 }
 
 }  // namespace
@@ -154,7 +261,13 @@ int pipck_txq_create(pipck_ctx* ctx, pipck_txq** out) {
     pipck_txq* q = new pipck_txq();
     q->ctx = ctx;
     q->device = dev;
-    PIPCK_HIP(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
+    if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&q->done, hipEventDisableTiming) != hipSuccess) {
+        set_error("pipck_txq_create: stream/event creation failed");
+        if (q->stream) (void)hipStreamDestroy(q->stream);
+        delete q;
+        return PIPCK_EHIP;
+    }
     *out = q;
     return PIPCK_OK;
 }
@@ -165,10 +278,9 @@ int pipck_txq_destroy(pipck_txq* q) {
         (void)hipStreamSynchronize(q->stream);
         (void)hipStreamDestroy(q->stream);
     }
-    q->bytes.release();
-    q->meta.release();
-    q->d_all.release();
-    q->d_work.release();
+    if (q->done) (void)hipEventDestroy(q->done);
+    q->batch[0].release();
+    q->batch[1].release();
     delete q;
     return PIPCK_OK;
 }
@@ -206,82 +318,41 @@ int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_fie
         set_error("pipck_txq_add_ip: header longer than 65535 bytes");
         return PIPCK_ERANGE;
     }
+    TxBatch* b = &q->batch[q->cur];
     uint64_t off = 0;
-    int rc = append_bytes(q, hdr, len, &off);
+    int rc = append_bytes(b, hdr, len, &off);
     if (rc) return rc;
-    q->ip_hdrs.push_back(pipck_desc{off, len, 0});
-    q->ip_field.push_back((uint8_t*)csum_field);
+    b->ip_hdrs.push_back(pipck_desc{off, len, 0});
+    b->ip_field.push_back((uint8_t*)csum_field);
     return PIPCK_OK;
 }
 
-uint64_t pipck_txq_pending(const pipck_txq* q) { return q ? q->inet_field.size() + q->ip_field.size() : 0; }
+uint64_t pipck_txq_pending(const pipck_txq* q) { return q ? q->batch[q->cur].pending() : 0; }
+
+uint64_t pipck_txq_inflight(const pipck_txq* q) { return q && q->inflight ? q->batch[q->cur ^ 1].pending() : 0; }
+
+int pipck_txq_submit(pipck_txq* q) {
+    if (!q) return PIPCK_EINVAL;
+    return on_device(q, [&] {
+        int rc = complete_inflight(q);  // at most one batch in flight
+        if (rc) return rc;
+        TxBatch* b = &q->batch[q->cur];
+        if (!b->pending()) return PIPCK_OK;
+        if ((rc = enqueue(q, b))) return rc;
+        q->inflight = true;
+        q->cur ^= 1;
+        return PIPCK_OK;
+    });
+}
+
+int pipck_txq_complete(pipck_txq* q) {
+    if (!q) return PIPCK_EINVAL;
+    return on_device(q, [&] { return complete_inflight(q); });
+}
 
 int pipck_txq_flush(pipck_txq* q) {
-    if (!q) return PIPCK_EINVAL;
-    const uint64_t n_in = q->inet_field.size(), n_ip = q->ip_field.size(), n_seg = q->inet_segs.size();
-    if (n_in + n_ip == 0) return PIPCK_OK;
-    int prev = 0;
-    PIPCK_HIP(hipGetDevice(&prev));
-    if (prev != q->device) PIPCK_HIP(hipSetDevice(q->device));
-    // meta layout (each part 16-byte aligned): inet segs | inet begin | pseudo recs | flow ids | ip descs | results
-    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    const size_t o_segs = 0, o_begin = al(o_segs + n_seg * sizeof(pipck_desc));
-    const size_t o_rec = al(o_begin + (n_in + 1) * sizeof(uint64_t));
-    const size_t o_flow = al(o_rec + n_in * sizeof(TxPseudo));
-    const size_t o_ip = al(o_flow + n_in * sizeof(uint32_t));
-    const size_t o_res = al(o_ip + n_ip * sizeof(pipck_desc));
-    const size_t meta_in = o_res, meta_all = al(o_res + (n_in + n_ip) * sizeof(uint16_t));
-    int rc = q->meta.reserve(meta_all);
-    if (rc) return rc;
-    uint8_t* m = q->meta.p;
-    if (n_seg) std::memcpy(m + o_segs, q->inet_segs.data(), n_seg * sizeof(pipck_desc));
-    std::memcpy(m + o_begin, q->inet_begin.data(), (n_in + 1) * sizeof(uint64_t));
-    if (n_in) std::memcpy(m + o_rec, q->inet_pseudo.data(), n_in * sizeof(TxPseudo));
-    uint32_t* flow = reinterpret_cast<uint32_t*>(m + o_flow);
-    for (uint64_t i = 0; i < n_in; i++) flow[i] = (uint32_t)i;  // packet i uses pseudo base i
-    if (n_ip) std::memcpy(m + o_ip, q->ip_hdrs.data(), n_ip * sizeof(pipck_desc));
-
-    const size_t nb = al(q->bytes.size);
-    if ((rc = q->d_all.reserve(nb + meta_all))) return rc;
-    if ((rc = q->d_work.reserve(al(n_in * 4) + al(std::max<uint64_t>(n_seg, 1) * 4) + 16))) return rc;
-    uint8_t* d_bytes = (uint8_t*)q->d_all.p;
-    uint8_t* d_meta = d_bytes + nb;
-    uint32_t* d_pseudo = (uint32_t*)q->d_work.p;
-    uint32_t* d_scratch = (uint32_t*)((uint8_t*)q->d_work.p + al(n_in * 4));
-    hipStream_t s = q->stream;
-    if (q->bytes.size) PIPCK_HIP(hipMemcpyAsync(d_bytes, q->bytes.p, q->bytes.size, hipMemcpyHostToDevice, s));
-    PIPCK_HIP(hipMemcpyAsync(d_meta, m, meta_in, hipMemcpyHostToDevice, s));
-    uint16_t* d_res = (uint16_t*)(d_meta + o_res);
-    if (n_in) {
-        hipLaunchKernelGGL(k_tx_pseudo, dim3((uint32_t)((n_in + 255) / 256)), dim3(256), 0, s,
-                           (const TxPseudo*)(d_meta + o_rec), (uint32_t)n_in, d_pseudo);
-        PIPCK_LAUNCHED("k_tx_pseudo");
-        rc = pipck_checksum_chains(d_bytes, (const pipck_desc*)(d_meta + o_segs), n_seg,
-                                   (const uint64_t*)(d_meta + o_begin), (const uint32_t*)(d_meta + o_flow), n_in,
-                                   d_pseudo, d_scratch, d_res, nullptr, s);
-        if (rc) return rc;
-    }
-    if (n_ip) {
-        rc = pipck_checksum_ragged(d_bytes, (const pipck_desc*)(d_meta + o_ip), n_ip, nullptr, d_res + n_in, nullptr, s);
-        if (rc) return rc;
-    }
-    PIPCK_HIP(hipMemcpyAsync(m + o_res, d_res, (n_in + n_ip) * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-    PIPCK_HIP(hipStreamSynchronize(s));
-    const uint16_t* res = reinterpret_cast<const uint16_t*>(m + o_res);
-    for (uint64_t i = 0; i < n_in + n_ip; i++) {  // htons(result) into the field (pip_tcp_packet.cpp:132-133)
-        uint8_t* f = i < n_in ? q->inet_field[i] : q->ip_field[i - n_in];
-        f[0] = (uint8_t)(res[i] >> 8);
-        f[1] = (uint8_t)res[i];
-    }
-    q->bytes.size = 0;
-    q->inet_segs.clear();
-    q->inet_begin.assign(1, 0);
-    q->inet_pseudo.clear();
-    q->inet_field.clear();
-    q->ip_hdrs.clear();
-    q->ip_field.clear();
-    if (prev != q->device) PIPCK_HIP(hipSetDevice(prev));
-    return PIPCK_OK;
+    int rc = pipck_txq_submit(q);
+    return rc ? rc : pipck_txq_complete(q);
 }
 
 }  // extern "C"

@@ -36,8 +36,10 @@ def test_pip_stack_on_amd_checksum_is_byte_identical():
     diff = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert not diff and len(got) == len(want), diff[:5]
     # the deferred (batched) API on real pip_buf chains, flushed in one GPU batch
-    line = [ln for ln in r.stderr.splitlines() if ln.startswith("DEFERRED")]
-    assert line, r.stderr[-2000:]
-    f = line[-1].split()
-    assert f[f.index("bad") + 1] == "0" and f[f.index("pending_after") + 1] == "0", line
-    assert int(f[f.index("checked") + 1]) >= 40
+    # and pipelined: submitted every 5 packets while the next are queued, then completed
+    lines = [ln for ln in r.stderr.splitlines() if ln.startswith("DEFERRED")]
+    assert [ln.split()[2] for ln in lines] == ["flush", "pipelined"], r.stderr[-2000:]
+    for line in lines:
+        f = line.split()
+        assert f[f.index("bad") + 1] == "0" and f[f.index("pending_after") + 1] == "0", line
+        assert int(f[f.index("checked") + 1]) >= 40

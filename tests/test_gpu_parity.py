@@ -621,3 +621,53 @@ def test_txq_mixed_batches_vs_oracle(oracle):
     finally:
         lib.pipck_txq_destroy(q)
         lib.pipck_ctx_destroy(ctx)
+
+
+def test_txq_submit_complete_pipeline(oracle):
+    """Double-buffered async flush: batches submitted while the next one fills,
+    fields written at the following submit/complete; a reused queue; flush
+    after submit; empty submits."""
+    lib = _lib.load()
+    ctx, q = C.c_void_p(), C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    rng = np.random.default_rng(1234)
+    try:
+        _lib.check("empty submit", lib.pipck_txq_submit(q))
+        _lib.check("empty complete", lib.pipck_txq_complete(q))
+        n_batches, per = 7, 333
+        fields = (C.c_uint8 * (2 * n_batches * per))()
+        keep, want = [], []
+        for bi in range(n_batches):
+            for i in range(per):
+                k = bi * per + i
+                segs = [rng.integers(0, 256, 20, dtype=np.uint8).tobytes(),
+                        rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()]
+                arr = (_lib.HSeg * 2)()
+                for j, sgm in enumerate(segs):
+                    b = C.create_string_buffer(sgm, max(len(sgm), 1))
+                    keep.append(b)
+                    arr[j].ptr = C.cast(b, C.c_void_p)
+                    arr[j].len = len(sgm)
+                s, d = rng.bytes(4), rng.bytes(4)
+                _lib.check("add4", lib.pipck_txq_add4(q, arr, 2, 6, int.from_bytes(s, "little"),
+                                                      int.from_bytes(d, "little"),
+                                                      C.c_void_p(C.addressof(fields) + 2 * k)))
+                want.append(oracle.inet_checksum_chain(segs, 6, s, d))
+            assert lib.pipck_txq_pending(q) == per
+            if bi == 3:
+                _lib.check("flush", lib.pipck_txq_flush(q))  # completes the in-flight batch and this one
+                assert lib.pipck_txq_inflight(q) == 0
+            else:
+                _lib.check("submit", lib.pipck_txq_submit(q))
+                assert lib.pipck_txq_pending(q) == 0 and lib.pipck_txq_inflight(q) == per
+                # every batch before this one is already stored
+                got = np.frombuffer(bytes(fields), dtype=">u2")[:bi * per]
+                assert np.array_equal(got, np.array(want[:bi * per], dtype=np.uint16)), bi
+        _lib.check("complete", lib.pipck_txq_complete(q))
+        assert lib.pipck_txq_inflight(q) == 0
+        got = np.frombuffer(bytes(fields), dtype=">u2")
+        assert np.array_equal(got, np.array(want, dtype=np.uint16))
+    finally:
+        lib.pipck_txq_destroy(q)
+        lib.pipck_ctx_destroy(ctx)
