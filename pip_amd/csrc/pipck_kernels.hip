@@ -395,6 +395,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
 }
 
 // ---------------------------------------------------------------------------
+// flat-stream kernel for short fixed strides (16-byte multiples below 1 KiB)
+// ---------------------------------------------------------------------------
+// The k_flat stream (a wave task of consecutive packets read as 1 KiB rows, a
+// ring of U rows in flight) for packets shorter than a row: a row now holds
+// several packet boundaries.  Each lane tracks its chunk's packet and
+// chunk-in-packet incrementally (64 chunks per row = q packets + rm chunks:
+// no divisions), and a row reduces by packet with the head/tail prefix trick
+// of the ragged kernel: the lane holding a packet's last chunk in the row adds
+// its inclusive DPP prefix, the lane holding its first chunk (unless lane 0)
+// subtracts its exclusive one, into the packet's LDS partial.
+struct LanePos {
+    uint32_t pkt, k;  // this lane's packet (within the task) and chunk-in-packet
+    __device__ __forceinline__ void advance(uint32_t q, uint32_t rm, uint32_t cpp) {
+        k += rm;
+        pkt += q;
+        if (k >= cpp) {
+            k -= cpp;
+            pkt++;
+        }
+    }
+};
+
+constexpr uint32_t kFlatSmallMaxRun = 1024;  // packets per wave task (LDS partials)
+
+template <int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_small(
+    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
+    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    __shared__ uint32_t s_res[4][kFlatSmallMaxRun];
+    const int lane = threadIdx.x & 63;
+    uint32_t* res = s_res[threadIdx.x >> 6];
+    const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
+    const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
+    const uint32_t lterm = len_term(len);
+    const uint32_t q = 64u / cpp, rm = 64u % cpp;
+    const uint64_t n_tasks = (n + run - 1) / run;
+    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kXcdGroups) != 0);
+    for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
+        const uint64_t p0 = task * run;
+        const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
+        const uint32_t tchunks = np * cpp;
+        const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
+        for (uint32_t i = lane; i < np; i += 64) res[i] = 0;
+        wave_sync();
+        LanePos lp{(uint32_t)lane / cpp, (uint32_t)lane % cpp};
+        LanePos pp = lp;
+        u32x4 v[U];
+        auto load_row = [&](u32x4& x, uint32_t rs) {
+            uint32_t c = rs + lane;
+            if (lp.k >= nch) c -= lp.k - nch + 1;  // padding: re-read the packet's last data chunk (masked)
+            x = NT ? load_stream(tb + min(c, tchunks - 1)) : load_plain(tb + min(c, tchunks - 1));
+            lp.advance(q, rm, cpp);
+        };
+#pragma unroll
+        for (int u = 0; u < U; u++) load_row(v[u], u * 64);
+        for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rs = r0 + u * 64;
+                if (rs < tchunks) {  // wave-uniform
+                    const bool active = rs + lane < tchunks;
+                    u32x4 x = v[u];
+                    if (!active || pp.k >= nch) x = u32x4{0u, 0u, 0u, 0u};
+                    else if (pp.k == nch - 1 && tail < 16) x = mask_tail(x, tail);
+                    const uint32_t val = fold64(sum4(x));
+                    const uint32_t inc = wave_incl_scan(val);
+                    const bool t_ = active && (pp.k == cpp - 1 || lane == 63);
+                    const bool h_ = active && pp.k == 0 && lane > 0;
+                    if (t_ || h_) atomicAdd(&res[pp.pkt], (t_ ? inc : 0u) - (h_ ? inc - val : 0u));
+                }
+                pp.advance(q, rm, cpp);
+                load_row(v[u], rs + 64 * U);  // ring: unconditional (clamped) reload
+            }
+        }
+        wave_sync();
+        uint32_t flow = 0;
+        const uint32_t fstep = pseudo && !flow_of ? 64u % n_flows : 0u;
+        if (pseudo && !flow_of) flow = (uint32_t)((flow_origin + p0 + lane) % n_flows);
+        for (uint32_t i = lane; i < np; i += 64) {
+            const uint64_t pkt = p0 + i;
+            const uint32_t F = bswap16(fold16(res[i]));  // packets start 16-byte aligned: even address
+            uint32_t P = 0;
+            if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : flow] + lterm;
+            if (VERIFY)
+                ok[pkt] = fold16(P + F) == 0xFFFFu;
+            else
+                out[pkt] = finish(P, F);
+            flow += fstep;
+            if (flow >= n_flows) flow -= n_flows;
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ragged / chain-segment kernel
 // ---------------------------------------------------------------------------
 struct RaggedTileLds {
@@ -803,6 +899,8 @@ static const SmallVariant& small_variant() {
     return kSmall[k >= 1 && k <= 4 ? k - 1 : 0];
 }
 
+constexpr uint32_t kNoFlatSmall = 128u;  // pipck_tune flags bit 7: never the short-stride flat kernel
+
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
@@ -824,6 +922,10 @@ static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_
                                     PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
                                     PIPCK_F(16, true)};
 #undef PIPCK_F
+static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
+    {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
+    {k_flat_small<16, true, false>, k_flat_small<16, true, true>}};
+
 static const FlatVariant& flat_variant(uint32_t loads) {
     switch (loads) {
         case 2: return kFlat[0];
@@ -903,6 +1005,23 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");
+        return PIPCK_OK;
+    }
+    // Short aligned strides from 64 B: the row stream with several packets per
+    // row (uniform 64/128/512-B packets: 6.0/5.8/6.1 TB/s vs 4.5/4.6/5.5 per
+    // packet; below 64 B k_small's lane-per-packet is 3-8 % faster,
+    // profiles/r01_ragged_shapes3.jsonl)
+    if (aligned && !g_tune.lanes.load() && !(g_tune.flags.load() & kNoFlatSmall) && stride >= 64 && stride < 64 * 16 &&
+        len <= stride) {
+        const uint32_t cpp = (uint32_t)(stride / 16);
+        const uint32_t flags = g_tune.flags.load();
+        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 64u;
+        const uint32_t run = std::min(kFlatSmallMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
+        const uint64_t tasks = (n + run - 1) / run;
+        hipLaunchKernelGGL(kFlatSmall[verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), 0,
+                           as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
+                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+        PIPCK_LAUNCHED("k_flat_small");
         return PIPCK_OK;
     }
     // Largest in-chunk offset any packet start can have: starts are

@@ -260,6 +260,50 @@ def test_small_packet_kernel_vs_oracle(oracle, misalign):
         engine.tune()
 
 
+@pytest.mark.parametrize("blocks", [0, 1, 9])
+def test_short_stride_flat_kernel_vs_oracle(oracle, blocks):
+    """k_flat_small (aligned arena, 16-byte-multiple strides below 1 KiB): many
+    packet boundaries per row, padding chunks, empty packets, partial tasks,
+    grid-stride tasks, RX verify, explicit flows; k_fixed/k_small (the
+    fallback with flat_small=False) must agree."""
+    rng = np.random.default_rng(900 + blocks)
+    try:
+        for stride in (16, 32, 48, 64, 80, 128, 144, 496, 512, 1008):  # < 64: the k_small fallback
+            for length in sorted({0, 1, stride // 2 + 1, stride - 15, stride - 1, stride} - {-15}):
+                if length < 0:
+                    continue
+                n = int(rng.choice([1, 63, 64, 65, 1000, 5000]))
+                fam = int(rng.choice([0, 4, 6]))
+                host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+                if n > 3:
+                    host[stride:2 * stride] = 0xFF
+                    host[2 * stride:3 * stride] = 0
+                _, arena = upload(host, 0)
+                seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
+                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+                engine.tune(blocks=blocks)
+                got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                assert np.array_equal(got, want), (stride, length, n, fam, np.nonzero(got != want)[0][:5])
+                ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
+                assert np.array_equal(ok.astype(bool), got == 0)
+                engine.tune(flat_small=False)
+                assert np.array_equal(u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None,
+                                                                origin)), want)
+        n, stride = 2001, 96
+        host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+        _, arena = upload(host, 0)
+        _, pseudo = engine.gen_flows(6, N_FLOWS, 5, 17)
+        flow_of = rng.integers(0, N_FLOWS, n).astype(np.int32)
+        engine.tune(blocks=blocks)
+        got = u16(engine.checksum_fixed(arena, stride, 90, n, pseudo, N_FLOWS, torch.from_numpy(flow_of).to(DEV), 0))
+        for i in range(0, n, 11):
+            s, d = oracle.flow6(5, int(flow_of[i]))
+            assert got[i] == oracle.inet6_checksum(host[i * stride:i * stride + 90].tobytes(), 17, s, d)
+    finally:
+        engine.tune()
+
+
 def test_fixed_grid_stride_loop(oracle):
     """Force a tiny grid so every block loops over many packets."""
     rng = np.random.default_rng(5)

@@ -25,7 +25,8 @@ from pip_amd.workloads import CFG4, N_FLOWS  # noqa: E402
 from size_scan import timed  # noqa: E402
 
 SHAPES = [("uniform_8980", 8980, 2 << 20), ("uniform_1480", 1480, 8 << 20), ("uniform_512", 512, 16 << 20),
-          ("uniform_128", 128, 32 << 20), ("zipf_cfg4", 0, 8 << 20), ("zipf_cfg4_32M", 0, 32 << 20)]
+          ("uniform_128", 128, 32 << 20), ("uniform_64", 64, 64 << 20), ("uniform_40", 40, 64 << 20),
+          ("uniform_20", 20, 128 << 20), ("zipf_cfg4", 0, 8 << 20), ("zipf_cfg4_32M", 0, 32 << 20)]
 
 
 def main():
@@ -45,7 +46,16 @@ def main():
         arms = {"ragged": lambda: engine.checksum_ragged(arena, desc, pseudo)}
         if length:
             stride = (length + 15) // 16 * 16
-            arms["fixed"] = lambda: engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS)
+
+            def fixed(**kw):
+                engine.tune(**kw)
+                try:
+                    return engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS)
+                finally:
+                    engine.tune()
+            arms["fixed"] = fixed
+            if stride < 1024:  # short strides: the row-stream kernel vs the per-packet ones
+                arms["fixed_no_flat_small"] = lambda: fixed(flat_small=False)
         res, ref = {}, None
         for _ in range(5):
             for k, fn in arms.items():
@@ -53,7 +63,7 @@ def main():
                 out = fn()
                 if ref is None:
                     ref = out.clone()
-                elif k == "fixed":
+                elif k.startswith("fixed"):
                     # fixed-path flows are (origin + i) % n_flows, the same as gen_ragged's descriptors
                     assert torch.equal(out, ref), name
         for k, ms in res.items():
