@@ -739,14 +739,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
     __shared__ RaggedTileLds s_tile[WPB];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RaggedTileLds& t = s_tile[w];
-    const uint32_t tpw = (kflags >> 16) & 0xFFu;  // consecutive tiles per wave (0: one window, see xcd_tasks)
-    TaskRange tr;
-    if (tpw) {
-        const uint64_t first = ((uint64_t)blockIdx.x * WPB + w) * tpw;
-        tr = {first, min(first + tpw, (n + 63) / 64), 1};
-    } else {
-        tr = xcd_tasks<WPB>((n + 63) / 64, (kflags & kXcdGroups) != 0);
-    }
+    const TaskRange tr = xcd_tasks<WPB>((n + 63) / 64, (kflags & kXcdGroups) != 0);
     uint64_t tile = tr.first;
     pipck_desc dn = pipck_desc{0, 0, 0};
     if (tile < tr.end && tile * 64 + lane < n) dn = desc[tile * 64 + lane];
@@ -1054,13 +1047,13 @@ static void launch_ragged_k(bool wide, uint64_t tiles, hipStream_t s, const uint
                             uint32_t f) {
     // one tile per wave: the in-order dispatcher hands out tiles as waves finish
     // (measured best, profiles/r01_size_scan*.jsonl)
-    const uint32_t tpw = (f >> 16) & 0xFFu;
-    const uint64_t waves = tpw ? (tiles + tpw - 1) / tpw : tiles;
+    // (runs of 2-4 consecutive tiles per wave measured 2-5 % slower,
+    // profiles/r01_ragged_tpw_scan.jsonl)
     if (wide)
-        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(tpw ? (uint32_t)((waves + 3) / 4) : grid_for(4, tiles, 0)),
+        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(grid_for(4, tiles, 0)),
                            dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
     else
-        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(tpw ? (uint32_t)waves : grid_for(1, tiles, 0)),
+        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(grid_for(1, tiles, 0)),
                            dim3(64), 0, s, a, d, n, ps, out, fseg, ok, err, f);
 }
 

@@ -37,6 +37,26 @@ def main():
     engine.require_gpu()
     w = CFG4
     pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
+    for payload, n in ((1460, 8 << 20), (8960, 2 << 20)):
+        # pip's TX chain shape: [20-B TCP header][payload] per packet, segments 16-B aligned
+        name = f"chain_tcp_{payload}"
+        if a.only and name not in a.only.split(","):
+            continue
+        slot = 32 + (payload + 15) // 16 * 16
+        arena = torch.randint(0, 256, (n * slot,), dtype=torch.uint8, device="cuda")
+        base = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+        segs = torch.empty((2 * n, 2), dtype=torch.int64, device="cuda")
+        segs[0::2, 0], segs[1::2, 0] = base, base + 32
+        segs[0::2, 1], segs[1::2, 1] = 20, payload  # len in the low u32, flow 0 in the high one
+        seg_begin = torch.arange(0, 2 * n + 1, 2, dtype=torch.int64, device="cuda")
+        pkt_flow = (torch.arange(n, dtype=torch.int64, device="cuda") % N_FLOWS).to(torch.int32)
+        run = lambda: engine.checksum_chains(arena, segs, seg_begin, pkt_flow, pseudo)  # noqa: E731
+        ms = statistics.median(timed(run, a.iters) for _ in range(5))
+        nbytes = (20 + payload + 2) * n
+        print(json.dumps({"shape": name, "packets": n, "gbytes": round(nbytes / 1e9, 2), "path": "chains",
+                          "ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1)}), flush=True)
+        del arena, segs, seg_begin, pkt_flow, base
+        torch.cuda.empty_cache()
     for name, length, n in SHAPES:
         if a.only and name not in a.only.split(","):
             continue
