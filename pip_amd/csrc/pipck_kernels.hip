@@ -788,7 +788,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
                 else
                     out[seg] = bad ? (uint16_t)0 : finish(P, F);
             } else {
-                fseg[seg] = F;
+                fseg[seg] = (len << 16) | F;  // len <= 65535 (bad segments: len 0, flagged in err)
             }
             if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
         }
@@ -796,16 +796,18 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
     }
 }
 
-__global__ void k_chain_finish(const pipck_desc* __restrict__ segs, const uint64_t* __restrict__ seg_begin,
-                               const uint32_t* __restrict__ pkt_flow, uint64_t n_pkts,
-                               const uint32_t* __restrict__ pseudo, const uint32_t* __restrict__ fseg,
-                               uint16_t* __restrict__ out) {
+// Per packet: the segments' folded sums and lengths, packed by k_ragged as
+// (len << 16) | F, so no descriptor is read again.
+__global__ void k_chain_finish(const uint64_t* __restrict__ seg_begin, const uint32_t* __restrict__ pkt_flow,
+                               uint64_t n_pkts, const uint32_t* __restrict__ pseudo,
+                               const uint32_t* __restrict__ fseg, uint16_t* __restrict__ out) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pkts) return;
     uint32_t total_len = 0, F = 0;  // pip_buf::total_len is a u32 (pip/pip_buf.h:17)
     for (uint64_t s = seg_begin[p], e = seg_begin[p + 1]; s < e; s++) {
-        total_len += segs[s].len;
-        F += fseg[s];
+        const uint32_t x = fseg[s];
+        total_len += x >> 16;
+        F += x & 0xFFFFu;
     }
     const uint32_t P = pseudo ? pseudo[pkt_flow ? pkt_flow[p] : 0u] + len_term(total_len) : 0u;
     out[p] = finish(P, F);
@@ -1185,7 +1187,7 @@ int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_
         int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s);
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_segs, d_seg_begin,
+    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_seg_begin,
                        d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out);
     PIPCK_LAUNCHED("k_chain_finish");
     return PIPCK_OK;
