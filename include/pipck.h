@@ -150,7 +150,8 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
  * addressing in the ragged kernel, bit 5 = 4-wave ragged blocks (default 1),
  * bit 6 = never the small-packet kernel (packets <= 64 B incl. chunk offset),
  * bit 7 = never the short-stride flat kernel (16-B-multiple strides < 1 KiB),
- * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bits 24..27 =
+ * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bit 16 = no
+ * lane-per-segment path for ragged tiles of tiny segments, bits 24..27 =
  * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 

@@ -502,6 +502,11 @@ struct RaggedTileLds {
 };
 
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
+// A tile whose segments all span <= 2 chunks (20-B IPv4 headers) is summed
+// lane-per-segment: 1.36 -> 1.69 TB/s on 20-B segments; at 3 chunks (40 B)
+// the chunk stream is 3 % faster (profiles/r01_ragged_shapes6_tiny.jsonl).
+constexpr uint32_t kTinyChunks = 2;
+constexpr uint32_t kNoTinyTiles = 1u << 16;  // pipck_tune flags bit 16: tiny tiles take the chunk stream too
 
 // Lane 0's value of a 64-bit quantity, as a scalar (both halves zero-extended).
 __device__ __forceinline__ uint64_t first_lane_u64(uint64_t x) {
@@ -755,32 +760,54 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         const uintptr_t addr = (uintptr_t)arena + d.offset;
         const uint32_t head = (uint32_t)(addr & 15);
         const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
-        const uint32_t incl = wave_incl_scan(nch);
-        const uint32_t total = __shfl(incl, 63, 64);
-        t.pre[lane] = incl - nch;
-        if (lane == 63) t.pre[64] = incl;
-        t.span[lane] = ((head + len) << 4) | head;
-        t.base[lane] = addr - head;
-        t.acc[lane] = 0;
-        t.mark[lane] = 0;
-        // Packed tile: every segment starts 16-byte aligned right where the
-        // previous one's chunks end (the layout of pip's TX batches and of the
-        // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
-        const uint64_t next_off = (uint64_t)__shfl_down((long long)d.offset, 1, 64);
-        const bool link = lane == 63 || seg + 1 >= n || d.offset + 16ull * nch == next_off;
-        const bool packed = (kflags & kNoPackedTiles) == 0 && __all(head == 0 && link);
-        const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
-        wave_sync();
-        uint64_t racc = 0;
-        uint32_t rseg = kNoSeg;
-        if (packed)
-            ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
-        else  // fewer rows in flight: the lookup path needs a segment register per row
-            ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
-        ragged_flush(t, lane, racc, rseg);
-        wave_sync();
+        uint32_t le_sum;
+        if (__all(nch <= kTinyChunks) && !(kflags & kNoTinyTiles)) {
+            // Tiny-segment tile (IPv4 headers, bare TCP/UDP headers): every lane
+            // sums its own segment with its loads all in flight; no chunk stream.
+            const u32x4* b = reinterpret_cast<const u32x4*>(addr - head);
+            u32x4 v[kTinyChunks];
+#pragma unroll
+            for (uint32_t j = 0; j < kTinyChunks; j++)
+                v[j] = j < nch ? (NT ? load_stream(b + j) : load_plain(b + j)) : u32x4{0u, 0u, 0u, 0u};
+            uint64_t acc = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kTinyChunks; j++) {
+                const int lo = j == 0 ? (int)head : 0;
+                const int hi = (int)(head + len) - 16 * (int)j;
+                u32x4 x = v[j];
+                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+                acc += sum4(x);
+            }
+            le_sum = fold64(acc);
+        } else {
+            const uint32_t incl = wave_incl_scan(nch);
+            const uint32_t total = __shfl(incl, 63, 64);
+            t.pre[lane] = incl - nch;
+            if (lane == 63) t.pre[64] = incl;
+            t.span[lane] = ((head + len) << 4) | head;
+            t.base[lane] = addr - head;
+            t.acc[lane] = 0;
+            t.mark[lane] = 0;
+            // Packed tile: every segment starts 16-byte aligned right where the
+            // previous one's chunks end (the layout of pip's TX batches and of the
+            // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
+            const uint64_t next_off = (uint64_t)__shfl_down((long long)d.offset, 1, 64);
+            const bool link = lane == 63 || seg + 1 >= n || d.offset + 16ull * nch == next_off;
+            const bool packed = (kflags & kNoPackedTiles) == 0 && __all(head == 0 && link);
+            const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
+            wave_sync();
+            uint64_t racc = 0;
+            uint32_t rseg = kNoSeg;
+            if (packed)
+                ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
+            else  // fewer rows in flight: the lookup path needs a segment register per row
+                ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
+            ragged_flush(t, lane, racc, rseg);
+            wave_sync();
+            le_sum = t.acc[lane];
+        }
         if (valid) {
-            const uint32_t F = bad ? 0u : be_fold(t.acc[lane], addr);
+            const uint32_t F = bad ? 0u : be_fold(le_sum, addr);
             if (FINAL) {
                 const uint32_t P = pseudo ? pseudo[d.flow] + len_term(len) : 0u;
                 if (ok)  // RX verification: valid iff the sum incl. the checksum field folds to 0xFFFF

@@ -431,6 +431,42 @@ def test_ragged_packed_tiles(oracle, rows):
         engine.tune()
 
 
+@pytest.mark.parametrize("misalign", [0, 3, 8])
+def test_ragged_tiny_segment_tiles(oracle, misalign):
+    """Tiles whose segments all span <= 2 chunks take the lane-per-segment path
+    (20-B IPv4 headers): tiles of 0..16-byte segments at 16-byte slots (plus
+    the arena misalignment), tiles of 0..49 bytes at random offsets (chunk
+    stream), long segments; the chunk stream alone (tiny_tiles=False) must agree."""
+    rng = np.random.default_rng(70 + misalign)
+    n = 64 * 30 + 17
+    lens = rng.integers(0, 50, n).astype(np.uint32)
+    tiny = np.arange(n) < 64 * 12  # first 12 tiles: every segment fits 2 chunks
+    lens[tiny] = rng.integers(0, 17, int(tiny.sum()))
+    lens[64 * 5:64 * 5 + 3] = 16
+    lens[64 * 20:64 * 21] = rng.integers(0, 3000, 64)  # a tile with long segments
+    lens[64 * 22 + 3] = 65535
+    offs = np.zeros(n, dtype=np.uint64)
+    pos = 0
+    for i in range(n):
+        pos = (pos + 15) // 16 * 16 if tiny[i] else pos + int(rng.integers(0, 20))
+        offs[i] = pos
+        pos += int(lens[i])
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    _, arena = upload(host, misalign)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, 11, 6)
+    desc = engine.make_desc(offs, lens, np.arange(n) % N_FLOWS)
+    want = oracle.batch_ragged(host, offs, lens, 4, 6, 11, N_FLOWS, 0)
+    try:
+        for tiny in (True, False):
+            engine.tune(tiny_tiles=tiny)
+            got = u16(engine.checksum_ragged(arena, desc, pseudo))
+            assert np.array_equal(got, want), (tiny, np.nonzero(got != want)[0][:5])
+            ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy().astype(bool)
+            assert np.array_equal(ok, got == 0)
+    finally:
+        engine.tune()
+
+
 def test_ragged_out_of_domain_flags_error(oracle):
     rng = np.random.default_rng(9)
     host = rng.integers(0, 256, 200_000, dtype=np.uint8)

@@ -64,6 +64,14 @@ def main():
         arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS, lengths=lengths)
         nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
         arms = {"ragged": lambda: engine.checksum_ragged(arena, desc, pseudo)}
+        if 0 < length <= 49:  # tiny segments: lane-per-segment tiles vs the chunk stream
+            def ragged_stream():
+                engine.tune(tiny_tiles=False)
+                try:
+                    return engine.checksum_ragged(arena, desc, pseudo)
+                finally:
+                    engine.tune()
+            arms["ragged_no_tiny"] = ragged_stream
         if length:
             stride = (length + 15) // 16 * 16
 
@@ -83,7 +91,7 @@ def main():
                 out = fn()
                 if ref is None:
                     ref = out.clone()
-                elif k.startswith("fixed"):
+                elif k.startswith("fixed") or k == "ragged_no_tiny":
                     # fixed-path flows are (origin + i) % n_flows, the same as gen_ragged's descriptors
                     assert torch.equal(out, ref), name
         for k, ms in res.items():
