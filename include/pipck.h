@@ -201,6 +201,12 @@ int pipck_host_sum(pipck_ctx* ctx, const pipck_hseg* segs, uint32_t nseg, uint32
 int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stride, uint32_t len,
                               uint64_t n_packets, int family, const void* h_flows, uint32_t n_flows,
                               uint64_t flow_origin, uint16_t* h_out);
+/* Per-packet path (pipck_host_sum): 0 = staged (H2D copy, kernel, D2H copy),
+ * 1 = zero-copy (the kernel reads the pinned, coherent staging buffer and
+ * writes the result to pinned host memory), 2 = auto (zero-copy up to 64 KiB
+ * of staged bytes; the default).  Process-wide; the initial mode comes from
+ * the environment variable PIPCK_HOST_ZERO_COPY (0/1/2). */
+void pipck_host_zero_copy(int mode);
 void* pipck_host_alloc(size_t bytes);   /* pinned host memory */
 void  pipck_host_free(void* p);
 

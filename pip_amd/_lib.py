@@ -72,6 +72,7 @@ SIGNATURES = {
     "pipck_txq_add_ip": (_i32, [_p, _p, _u32, _p]),
     "pipck_txq_pending": (_u64, [_p]),
     "pipck_txq_flush": (_i32, [_p]),
+    "pipck_host_zero_copy": (None, [_i32]),
     "pipck_txq_submit": (_i32, [_p]),
     "pipck_txq_complete": (_i32, [_p]),
     "pipck_txq_inflight": (_u64, [_p]),

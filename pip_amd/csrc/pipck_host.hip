@@ -11,6 +11,8 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -19,6 +21,14 @@
 namespace pipck {
 
 static thread_local std::string t_err;
+// pipck_host_sum path: staged copies (0), zero-copy host access (1), or
+// auto (2: zero-copy up to kZeroCopyMax staged bytes); initial value from
+// PIPCK_HOST_ZERO_COPY, default auto.
+static std::atomic<int> g_zero_copy{[] {
+    const char* e = getenv("PIPCK_HOST_ZERO_COPY");
+    return e && (*e == '0' || *e == '1') ? *e - '0' : 2;
+}()};
+constexpr size_t kZeroCopyMax = 64u << 10;
 void set_error(const std::string& msg) { t_err = msg; }
 
 int device_cus() {
@@ -136,7 +146,9 @@ int grow_stage(pipck_ctx* c, size_t need) {
     c->h_stage = nullptr;
     c->d_stage = nullptr;
     c->stage_cap = 0;
-    PIPCK_HIP(hipHostMalloc((void**)&c->h_stage, cap, hipHostMallocDefault));
+    // coherent (fine-grained): the zero-copy path's kernel reads it directly,
+    // and no device cache may hold a previous call's bytes
+    PIPCK_HIP(hipHostMalloc((void**)&c->h_stage, cap, hipHostMallocCoherent));
     PIPCK_HIP(hipMalloc((void**)&c->d_stage, cap));
     c->stage_cap = cap;
     return PIPCK_OK;
@@ -176,7 +188,7 @@ int pipck_ctx_create(int device, pipck_ctx** out) {
         PIPCK_HIP(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
     }
     PIPCK_HIP(hipMalloc((void**)&c->d_result, sizeof(uint32_t)));
-    PIPCK_HIP(hipHostMalloc((void**)&c->h_result, sizeof(uint32_t), hipHostMallocDefault));
+    PIPCK_HIP(hipHostMalloc((void**)&c->h_result, sizeof(uint32_t), hipHostMallocCoherent));
     *out = c;
     return PIPCK_OK;
 }
@@ -228,15 +240,27 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
         off += ((size_t)segs[i].len + 15) & ~(size_t)15;
     }
     hipStream_t s = c->stream[0];
-    if (need) PIPCK_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, need, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->d_stage + table,
-                       reinterpret_cast<const SegRef*>(c->d_stage), nseg, init, c->d_result);
-    PIPCK_LAUNCHED("k_exact_chain");
-    PIPCK_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    const int zc = g_zero_copy.load(std::memory_order_relaxed);
+    if (zc == 1 || (zc == 2 && need <= kZeroCopyMax)) {
+        // The kernel reads the pinned staging buffer over PCIe and writes the
+        // result into pinned host memory: no copy commands around the launch.
+        *c->h_result = 0xFFFFFFFFu;
+        hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->h_stage + table,
+                           reinterpret_cast<const SegRef*>(c->h_stage), nseg, init, c->h_result);
+        PIPCK_LAUNCHED("k_exact_chain");
+    } else {
+        if (need) PIPCK_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, need, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->d_stage + table,
+                           reinterpret_cast<const SegRef*>(c->d_stage), nseg, init, c->d_result);
+        PIPCK_LAUNCHED("k_exact_chain");
+        PIPCK_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    }
     PIPCK_HIP(hipStreamSynchronize(s));
-    *out = *c->h_result;
+    *out = *(volatile uint32_t*)c->h_result;
     return PIPCK_OK;
 }
+
+void pipck_host_zero_copy(int mode) { g_zero_copy.store(mode >= 0 && mode <= 2 ? mode : 2); }
 
 void* pipck_host_alloc(size_t bytes) {
     void* p = nullptr;

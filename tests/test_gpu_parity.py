@@ -66,13 +66,34 @@ class PcAdapter:
 # ----------------------------------------------------------------------------
 # 1. pip's known answers through the per-packet (exact) device path
 # ----------------------------------------------------------------------------
-def test_every_known_answer_on_gpu(kat):
+@pytest.fixture
+def staged_per_packet():
+    """The per-packet path with staged copies (the default auto mode zero-copies small calls)."""
+    lib = _lib.load()
+    lib.pipck_host_zero_copy(0)
+    yield
+    lib.pipck_host_zero_copy(2)
+
+
+def test_every_known_answer_on_gpu(kat, staged_per_packet):
     bad = []
     for c in kat:
         got = run_case(PcAdapter, c)
         if got != c["expect"]:
             bad.append((c["fn"], c.get("data", c.get("segs")), c["expect"], got))
     assert not bad, bad[:5]
+
+
+def test_every_known_answer_on_gpu_zero_copy(kat):
+    """The same known answers through the zero-copy per-packet path (the kernel
+    reads pinned host staging and writes the result to host memory)."""
+    lib = _lib.load()
+    lib.pipck_host_zero_copy(1)
+    try:
+        bad = [c["fn"] for c in kat if run_case(PcAdapter, c) != c["expect"]]
+        assert not bad, bad[:5]
+    finally:
+        lib.pipck_host_zero_copy(2)
 
 
 def test_per_packet_api_is_thread_safe(kat):
