@@ -5,17 +5,28 @@
 // reduction, HBM-read bound: no MFMA, no LDS tiling of the payload.  See
 // pipck_device.hpp for why summing little-endian dwords in any order is exact.
 //
-// Kernels
-//   k_fixed<G,NL>   fixed-stride batches (cfg2/3/5 shapes): a group of G lanes
-//                   per packet, NL 16-byte loads per lane in flight per pass,
-//                   64/G packets per wave, group reduce by cross-lane shuffles.
-//   k_ragged<FIN,U> ragged batches and chain segments (cfg4 shape): each wave
-//                   owns a tile of 64 segments and streams the tile's 16-byte
-//                   chunks flat and coalesced (U rows of 64 chunks in flight),
-//                   mapping chunk -> segment by binary search over the tile's
-//                   chunk prefix in LDS, and reducing by segment with a wave
-//                   prefix scan; per-segment partials accumulate in LDS.
-//   k_chain_finish  per-packet fold of chain-segment partials + pseudo-header.
+// Kernels (launch choice in launch_fixed / launch_ragged below)
+//   k_flat<U,PIPE>    fixed 16-B-multiple strides >= 1 KiB (cfg2/3/5): a wave
+//                     task of consecutive packets streamed as coalesced 1 KiB
+//                     rows, a ring of U rows in flight, <= 1 packet boundary
+//                     per row, one wave reduce per packet; one task per wave.
+//   k_flat_small<U>   fixed 16-B-multiple strides 64 B .. 1 KiB: the same row
+//                     stream with many packets per row, reduced by packet with
+//                     a DPP prefix scan into LDS partials.
+//   k_small<NL,K>     packets <= 64 B incl. their first chunk's offset (cfg1's
+//                     20-B headers): one lane per packet, every load of the
+//                     wave task in flight before the first reduce.
+//   k_fixed<G,NL>     the remaining fixed strides (unaligned medium packets):
+//                     G lanes per packet, group reduce by cross-lane shuffles.
+//   k_ragged<FIN,U,PIPE,NT,WPB>
+//                     ragged batches and chain segments (cfg4): a wave owns a
+//                     tile of 64 segments and streams its chunks as 1 KiB rows
+//                     (a ring of U in flight); packed tiles locate segments by
+//                     ballot + LDS marks + DPP max-scan, others by a search
+//                     over the tile's chunk prefix; rows reduce by segment with
+//                     a DPP prefix scan into LDS partials.  Tiles of <= 2-chunk
+//                     segments are summed lane-per-segment instead.
+//   k_chain_finish    per-packet fold of chain-segment partials + pseudo-header.
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
