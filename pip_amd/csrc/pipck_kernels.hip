@@ -270,15 +270,31 @@ __device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint32_t* r
     if (lane == 0) res[i] = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
 }
 
+// Pseudo-header bases of the task's packets (lane's packets i = lane, lane + 64),
+// loaded when the task starts: at its end they are already in registers, so
+// the wave's last act before exiting is a store, not a dependent table load.
+__device__ __forceinline__ void flat_pseudo(uint32_t (&P)[2], uint64_t p0, uint32_t np, const uint32_t* pseudo,
+                                            uint32_t n_flows, const uint32_t* flow_of, uint64_t flow_origin,
+                                            int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint32_t i = lane + 64u * j;
+        const uint64_t pkt = p0 + i;
+        P[j] = 0;
+        if (pseudo && i < np) P[j] = pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)];
+    }
+}
+
 template <bool VERIFY>
-__device__ __forceinline__ void flat_write(const uint32_t* res, uint64_t p0, uint32_t np, const uint32_t* pseudo,
-                                           uint32_t n_flows, const uint32_t* flow_of, uint64_t flow_origin,
-                                           uint32_t lterm, uint16_t* out, uint8_t* ok, int lane) {
-    for (uint32_t i = lane; i < np; i += 64) {
+__device__ __forceinline__ void flat_write(const uint32_t* res, uint64_t p0, uint32_t np, const uint32_t (&Pb)[2],
+                                           bool has_pseudo, uint32_t lterm, uint16_t* out, uint8_t* ok, int lane) {
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint32_t i = lane + 64u * j;
+        if (i >= np) continue;
         const uint64_t pkt = p0 + i;
         const uint32_t F = res[i];
-        uint32_t P = 0;
-        if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)] + lterm;
+        const uint32_t P = has_pseudo ? Pb[j] + lterm : 0u;
         if (VERIFY)
             ok[pkt] = fold16(P + F) == 0xFFFFu;
         else
@@ -382,6 +398,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
         const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
         uint64_t acc = 0;
         RowPos lp{0, 0}, pp{0, 0};
+        uint32_t Pb[2];
+        flat_pseudo(Pb, p0, np, pseudo, n_flows, flow_of, flow_origin, lane);
         u32x4 v[U];
         flat_load_rows<U, NT>(v, tb, 0, tchunks, lp, cpp, nch, lane);
         for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
@@ -400,7 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
         }
         flat_stash(acc, np - 1, res, lane);
         wave_sync();
-        flat_write<VERIFY>(res, p0, np, pseudo, n_flows, flow_of, flow_origin, lterm, out, ok, lane);
+        flat_write<VERIFY>(res, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane);
         wave_sync();
     }
 }
@@ -768,6 +786,8 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         if (tile + tr.step < tr.end) dn = nseg < n ? desc[nseg] : pipck_desc{0, 0, 0};
         const bool bad = valid && d.len > PIPCK_MAX_SEG_LEN;
         const uint32_t len = (valid && !bad) ? d.len : 0u;
+        // the flow's pseudo-header base, loaded now so the tile's end waits on nothing
+        const uint32_t Pbase = FINAL && pseudo && valid ? pseudo[d.flow] : 0u;
         const uintptr_t addr = (uintptr_t)arena + d.offset;
         const uint32_t head = (uint32_t)(addr & 15);
         const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
@@ -820,7 +840,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         if (valid) {
             const uint32_t F = bad ? 0u : be_fold(le_sum, addr);
             if (FINAL) {
-                const uint32_t P = pseudo ? pseudo[d.flow] + len_term(len) : 0u;
+                const uint32_t P = pseudo ? Pbase + len_term(len) : 0u;
                 if (ok)  // RX verification: valid iff the sum incl. the checksum field folds to 0xFFFF
                     ok[seg] = !bad && fold16(P + F) == 0xFFFFu;
                 else
