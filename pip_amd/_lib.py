@@ -11,7 +11,11 @@ import os
 from pathlib import Path
 
 LIB_DIR = Path(__file__).resolve().parent / "lib"
-LIBPIPCK = LIB_DIR / "libpipck.so"
+# PIPCK_LIB points a process at another build of the same ABI (tools/ab_scan.py
+# runs each build in its own process: two builds in one process would share
+# kernel symbol names, and the HIP runtime would launch one build's kernels
+# for both).
+LIBPIPCK = Path(os.environ.get("PIPCK_LIB") or LIB_DIR / "libpipck.so")
 LIBSHIM = LIB_DIR / "libpip_checksum_amd.so"
 
 PIPCK_OK, PIPCK_EINVAL, PIPCK_ERANGE, PIPCK_EHIP, PIPCK_ENODEV, PIPCK_ENOMEM = range(6)

@@ -260,46 +260,50 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
 }
 
-// A finished packet's folded big-endian sum goes to the wave's LDS slot; the
-// pseudo-header loads and the global stores wait for the task's end
-// (flat_write): on gfx9 both count in VM_CNT, so inside the row loop each
-// one would make the next row's wait drain every load in flight.
-constexpr uint32_t kFlatMaxRun = 128;  // packets per wave task
-__device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint32_t* res, int lane) {
-    const uint32_t s = wave_total(fold64(acc));
-    if (lane == 0) res[i] = bswap16(fold16(s));  // packet starts 16-byte aligned: even address
+// A finished packet is not reduced across the wave on the spot: every lane
+// parks its folded partial (16 bits keep the residue and zero-ness) in the
+// wave's LDS block, column-major (lane j's partial of packet i at j*pitch + i),
+// and flat_write sums packet i's 64 partials in lane i at the task's end.  A
+// per-packet DPP reduce cost ~27 issue slots (6 DPP adds with their wait
+// states, readlane, the scalar fold); this costs a fold and one ds_write_b16.
+// The pseudo-header loads and the global stores also wait for the task's end:
+// on gfx9 both count in VM_CNT, so inside the row loop each one would make the
+// next row's wait drain every load in flight.
+constexpr uint32_t kFlatMaxRun = 64;  // packets per wave task
+// u16 slots per lane row: >= run, and an odd number of dwords so the 64 lanes
+// of one ds_write_b16 land in distinct banks (mod 32)
+__host__ __device__ constexpr uint32_t flat_pitch(uint32_t run) {
+    return ((run + 1) / 2 % 2 ? (run + 1) / 2 : (run + 1) / 2 + 1) * 2;
+}
+__device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint16_t* part, uint32_t pitch, int lane) {
+    part[lane * pitch + i] = (uint16_t)fold16(fold64(acc));
 }
 
-// Pseudo-header bases of the task's packets (lane's packets i = lane, lane + 64),
-// loaded when the task starts: at its end they are already in registers, so
-// the wave's last act before exiting is a store, not a dependent table load.
-__device__ __forceinline__ void flat_pseudo(uint32_t (&P)[2], uint64_t p0, uint32_t np, const uint32_t* pseudo,
-                                            uint32_t n_flows, const uint32_t* flow_of, uint64_t flow_origin,
-                                            int lane) {
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t i = lane + 64u * j;
-        const uint64_t pkt = p0 + i;
-        P[j] = 0;
-        if (pseudo && i < np) P[j] = pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)];
-    }
+// Pseudo-header base of the task's packet `lane` (run <= 64), loaded when the
+// task starts: at its end it is already in a register, so the wave's last act
+// before exiting is a store, not a dependent table load.
+__device__ __forceinline__ uint32_t flat_pseudo(uint64_t p0, uint32_t np, const uint32_t* pseudo, uint32_t n_flows,
+                                                const uint32_t* flow_of, uint64_t flow_origin, int lane) {
+    const uint64_t pkt = p0 + lane;
+    if (!pseudo || (uint32_t)lane >= np) return 0u;
+    return pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)];
 }
 
 template <bool VERIFY>
-__device__ __forceinline__ void flat_write(const uint32_t* res, uint64_t p0, uint32_t np, const uint32_t (&Pb)[2],
-                                           bool has_pseudo, uint32_t lterm, uint16_t* out, uint8_t* ok, int lane) {
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t i = lane + 64u * j;
-        if (i >= np) continue;
-        const uint64_t pkt = p0 + i;
-        const uint32_t F = res[i];
-        const uint32_t P = has_pseudo ? Pb[j] + lterm : 0u;
-        if (VERIFY)
-            ok[pkt] = fold16(P + F) == 0xFFFFu;
-        else
-            out[pkt] = finish(P, F);
-    }
+__device__ __forceinline__ void flat_write(const uint16_t* part, uint32_t pitch, uint64_t p0, uint32_t np,
+                                           uint32_t Pb, bool has_pseudo, uint32_t lterm, uint16_t* out, uint8_t* ok,
+                                           int lane) {
+    if ((uint32_t)lane >= np) return;
+    uint32_t s = 0;
+#pragma unroll 16
+    for (int j = 0; j < 64; j++) s += part[j * pitch + lane];
+    const uint32_t F = bswap16(fold16(s));  // packets start 16-byte aligned: even address
+    const uint32_t P = has_pseudo ? Pb + lterm : 0u;
+    const uint64_t pkt = p0 + lane;
+    if (VERIFY)
+        ok[pkt] = fold16(P + F) == 0xFFFFu;
+    else
+        out[pkt] = finish(P, F);
 }
 
 // Row bookkeeping is incremental (cpp >= 64, so a row advances the packet by at
@@ -342,10 +346,14 @@ __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], const u32x4* tb, u
 // rs < tchunks (wave-uniform)
 __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
                                                 uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
-                                                uint32_t* res, int lane) {
+                                                uint16_t* part, uint32_t pitch, int lane) {
     if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
-        flat_stash(acc, pp.pkt - 1, res, lane);
+        flat_stash(acc, pp.pkt - 1, part, pitch, lane);
         acc = 0;
+    }
+    if (pp.k + 65 <= nch) {  // wave-uniform: 64 whole data chunks of one packet, none its last
+        acc += sum4(v);
+        return;
     }
     uint32_t k = pp.k + lane;
     if (k >= cpp) k -= cpp;
@@ -358,7 +366,7 @@ __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uin
         acc += val;
     } else {
         acc += lane < (int)b ? val : 0ull;
-        flat_stash(acc, pp.pkt, res, lane);
+        flat_stash(acc, pp.pkt, part, pitch, lane);
         acc = lane < (int)b ? 0ull : val;
     }
 }
@@ -366,11 +374,11 @@ __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uin
 template <int U>
 __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r0, uint32_t tchunks, RowPos& pp,
                                                  uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
-                                                 uint32_t* res, int lane) {
+                                                 uint16_t* part, uint32_t pitch, int lane) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t rs = r0 + u * 64;  // wave-uniform
-        if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
+        if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
         pp.advance(cpp);
     }
 }
@@ -383,9 +391,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
                                               uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
-    __shared__ uint32_t s_res[4][kFlatMaxRun];
+    extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16 (launch_fixed sizes it)
     const int lane = threadIdx.x & 63;
-    uint32_t* res = s_res[threadIdx.x >> 6];
+    const uint32_t pitch = flat_pitch(run);
+    uint16_t* part = s_part + (threadIdx.x >> 6) * 64u * pitch;
     const uint32_t nch = (len + 15) >> 4;                         // data chunks per packet (<= cpp)
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     const uint32_t lterm = len_term(len);
@@ -398,8 +407,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
         const u32x4* tb = reinterpret_cast<const u32x4*>(arena) + p0 * cpp;
         uint64_t acc = 0;
         RowPos lp{0, 0}, pp{0, 0};
-        uint32_t Pb[2];
-        flat_pseudo(Pb, p0, np, pseudo, n_flows, flow_of, flow_origin, lane);
+        const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, flow_origin, lane);
         u32x4 v[U];
         flat_load_rows<U, NT>(v, tb, 0, tchunks, lp, cpp, nch, lane);
         for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
@@ -407,18 +415,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t rs = r0 + u * 64;  // wave-uniform
-                    if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
+                    if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
                     pp.advance(cpp);
                     flat_load_row<NT>(v[u], tb, rs + 64 * U, tchunks, lp, cpp, nch, lane);  // unconditional (clamped)
                 }
             } else {
-                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, res, lane);
+                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
                 if (r0 + 64 * U < tchunks) flat_load_rows<U, NT>(v, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
             }
         }
-        flat_stash(acc, np - 1, res, lane);
+        flat_stash(acc, np - 1, part, pitch, lane);
         wave_sync();
-        flat_write<VERIFY>(res, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane);
+        flat_write<VERIFY>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane);
         wave_sync();
     }
 }
@@ -1054,7 +1062,8 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
-        hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), 0, as_stream(stream),
+        const size_t lds = 4u * 64u * flat_pitch(run) * sizeof(uint16_t);
+        hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");

@@ -1,81 +1,98 @@
 #!/usr/bin/env python3
-"""Same-process A/B of libpipck builds (box-to-box variation is a few %,
+"""A/B of libpipck builds on one GPU box (box-to-box variation is a few %,
 larger than most kernel changes).
 
-    python tools/ab_scan.py [--only cfg2,cfg4] pip_amd/lib/ab/libpipck_base.so [more.so ...]
+    python tools/ab_scan.py [--only cfg2,cfg4] [--rounds 3] pip_amd/lib/ab/libpipck_base.so [more.so ...]
 
 Each given library is an arm named after its file stem (minus "libpipck_"),
-arm "cur" = pip_amd/lib/libpipck.so; all run the same device batches
-(generated once), rounds interleaved, results checked equal.  One JSON line
-per (workload, arm).
+arm "cur" = pip_amd/lib/libpipck.so.  Every (round, arm) runs in its OWN
+process (PIPCK_LIB selects the build): two builds loaded into one process
+share kernel symbol names, and the HIP runtime then launches one build's
+kernels for both.  Rounds alternate the arms; each process generates the same
+device batches and reports the median kernel time; the results' hashes must
+agree across arms.  One JSON line per (workload, arm): median over rounds.
 """
 from __future__ import annotations
 
-import ctypes as C
+import argparse
+import hashlib
 import json
+import os
 import statistics
+import subprocess
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-
-import torch  # noqa: E402
-
-from pip_amd import _lib, engine  # noqa: E402
-from pip_amd.workloads import CFG2, CFG3, CFG4, CFG5, N_FLOWS  # noqa: E402
-from size_scan import timed  # noqa: E402
+ROOT = Path(__file__).resolve().parents[1]
+WORKLOADS = {"cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20}
 
 
-def bind(lib):
-    for name in ("pipck_checksum_fixed", "pipck_checksum_ragged"):
-        res, args = _lib.SIGNATURES[name]
-        fn = getattr(lib, name)
-        fn.restype, fn.argtypes = res, args
-    return lib
+def worker(only: list[str], iters: int) -> None:
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "tools"))
+    import torch
 
+    from pip_amd import engine
+    from pip_amd.workloads import BY_CFG, N_FLOWS
+    from size_scan import timed
 
-def main():
     engine.require_gpu()
-    args = sys.argv[1:]
-    only = None
-    if args and args[0] == "--only":
-        only, args = set(args[1].split(",")), args[2:]
-    libs = {Path(a).stem.replace("libpipck_", ""): bind(C.CDLL(str(Path(a).resolve()))) for a in args}
-    libs["cur"] = bind(_lib.load())
-    p = engine._ptr
-    for w, n in ((CFG2, 4 << 20), (CFG3, 1 << 20), (CFG5, 8 << 20), (CFG4, 8 << 20)):
-        if only and f"cfg{w.cfg}" not in only:
-            continue
+    for name in only:
+        w, n = BY_CFG[int(name[3:])], WORKLOADS[name]
         pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
-        out = torch.empty(n, dtype=torch.int16, device="cuda")
-        st = engine.current_stream()
         if w.ragged:
             arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
-            runs = {k: (lambda lib=lib: lib.pipck_checksum_ragged(p(arena), p(desc), n, p(pseudo), p(out), None, st))
-                    for k, lib in libs.items()}
+            run = lambda: engine.checksum_ragged(arena, desc, pseudo)  # noqa: E731
         else:
             arena = torch.empty(n * w.stride, dtype=torch.uint8, device="cuda")
             engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
             nbytes = (w.length + 2) * n
-            runs = {k: (lambda lib=lib: lib.pipck_checksum_fixed(p(arena), w.stride, w.length, n, p(pseudo),
-                                                                 N_FLOWS, None, 0, p(out), st))
-                    for k, lib in libs.items()}
-        res, ref = {}, None
-        for _ in range(7):
-            for k, fn in runs.items():
-                res.setdefault(k, []).append(timed(fn, 10))
-                out.zero_()
-                assert fn() == 0
-                if ref is None:
-                    ref = out.clone()
-                assert torch.equal(out, ref), k
-        for k, ms in res.items():
-            m = statistics.median(ms)
-            print(json.dumps({"workload": w.name, "packets": n, "arm": k, "ms": round(m, 4),
-                              "GBps": round(nbytes / m / 1e6, 1)}), flush=True)
+            run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
+        ms = statistics.median(timed(run, iters) for _ in range(3))
+        digest = hashlib.sha256(run().cpu().numpy().tobytes()).hexdigest()[:16]
+        print(json.dumps({"workload": w.name, "packets": n, "ms": ms, "bytes": nbytes, "sha": digest}), flush=True)
         del arena
         torch.cuda.empty_cache()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="cfg2,cfg3,cfg5,cfg4")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("libs", nargs="*")
+    a = ap.parse_args()
+    only = [x for x in a.only.split(",") if x]
+    if a.worker:
+        worker(only, a.iters)
+        return
+    arms = {Path(x).stem.replace("libpipck_", ""): str(Path(x).resolve()) for x in a.libs}
+    arms["cur"] = str(ROOT / "pip_amd" / "lib" / "libpipck.so")
+    res: dict[tuple[str, str], list[float]] = {}
+    meta: dict[str, dict] = {}
+    for rnd in range(a.rounds):
+        order = list(arms.items()) if rnd % 2 == 0 else list(reversed(arms.items()))
+        for arm, path in order:
+            env = dict(os.environ, PIPCK_LIB=path)
+            r = subprocess.run([sys.executable, __file__, "--worker", "--only", ",".join(only), "--iters",
+                                str(a.iters)], env=env, capture_output=True, text=True, timeout=600)
+            if r.returncode:
+                sys.stderr.write(r.stderr[-3000:])
+                raise SystemExit(f"arm {arm} failed (rc {r.returncode})")
+            for line in r.stdout.splitlines():
+                if not line.startswith("{"):
+                    continue
+                d = json.loads(line)
+                res.setdefault((d["workload"], arm), []).append(d["ms"])
+                m = meta.setdefault(d["workload"], {"bytes": d["bytes"], "packets": d["packets"], "sha": d["sha"]})
+                if m["sha"] != d["sha"]:
+                    raise SystemExit(f"{d['workload']}: arm {arm} results differ from the first arm's")
+    for (wl, arm), ms in res.items():
+        m = statistics.median(ms)
+        print(json.dumps({"workload": wl, "packets": meta[wl]["packets"], "arm": arm, "ms": round(m, 4),
+                          "GBps": round(meta[wl]["bytes"] / m / 1e6, 1), "rounds": len(ms)}), flush=True)
 
 
 if __name__ == "__main__":
