@@ -102,6 +102,8 @@ def load() -> C.CDLL:
             "(or __graft_entry__.build()); there is no CPU fallback")
     lib = C.CDLL(os.fspath(LIBPIPCK), mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("PIPCK_LIB") and not hasattr(lib, name):
+            continue  # an older build under A/B may predate some entry points
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
