@@ -207,7 +207,12 @@ int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stri
  * of staged bytes; the default).  Process-wide; the initial mode comes from
  * the environment variable PIPCK_HOST_ZERO_COPY (0/1/2). */
 void pipck_host_zero_copy(int mode);
-void* pipck_host_alloc(size_t bytes);   /* pinned host memory */
+void* pipck_host_alloc(size_t bytes);   /* pinned, coherent host memory (device-readable in place) */
+/* Pin an existing host range (a utun / socket buffer ring) so the GPU can read
+ * it in place at the same address; PIPCK_EINVAL if the runtime maps it to a
+ * different device address. */
+int pipck_host_register(void* p, size_t bytes);
+int pipck_host_unregister(void* p);
 void  pipck_host_free(void* p);
 
 /* ---- deferred TX queue -------------------------
@@ -229,6 +234,14 @@ int pipck_txq_add4(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t 
 /* pip_inet6_checksum_buf (pip_checksum.cpp:118-148): src/dst as in6_addr bytes */
 int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
                    const uint8_t* dst, void* csum_field);
+/* Zero-copy forms: the segments lie in pinned host memory (pipck_host_alloc or
+ * pipck_host_register) and are read by the GPU in place when the batch runs --
+ * nothing is copied at add time, so they must stay valid and unchanged until
+ * the batch completes (flush, or the complete/submit after its submit). */
+int pipck_txq_add4_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, uint32_t src,
+                      uint32_t dst, void* csum_field);
+int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
+                      const uint8_t* dst, void* csum_field);
 /* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);
 /* packets added since the last submit/flush */

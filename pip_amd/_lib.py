@@ -74,6 +74,10 @@ SIGNATURES = {
     "pipck_txq_add4": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _u32, _u32, _p]),
     "pipck_txq_add6": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _p, _p, _p]),
     "pipck_txq_add_ip": (_i32, [_p, _p, _u32, _p]),
+    "pipck_txq_add4_zc": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _u32, _u32, _p]),
+    "pipck_txq_add6_zc": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _p, _p, _p]),
+    "pipck_host_register": (_i32, [_p, _sz]),
+    "pipck_host_unregister": (_i32, [_p]),
     "pipck_txq_pending": (_u64, [_p]),
     "pipck_txq_flush": (_i32, [_p]),
     "pipck_host_zero_copy": (None, [_i32]),

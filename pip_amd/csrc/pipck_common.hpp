@@ -35,4 +35,11 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // Number of CUs on the current device (cached per device).
 int device_cus();
 
+// pipck_checksum_chains without argument checks, for callers whose segment
+// descriptors hold absolute device-accessible addresses (d_arena == nullptr):
+// the TX queue mixes its device staging copy with zero-copy pinned host segments.
+int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
+                     const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo, uint32_t* d_scratch,
+                     uint16_t* d_out, uint32_t* d_err, hipStream_t s);
+
 }  // namespace pipck

@@ -262,9 +262,31 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
 
 void pipck_host_zero_copy(int mode) { g_zero_copy.store(mode >= 0 && mode <= 2 ? mode : 2); }
 
+int pipck_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) {
+        set_error("pipck_host_register: null pointer or empty range");
+        return PIPCK_EINVAL;
+    }
+    PIPCK_HIP(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || dp != p) {
+        (void)hipHostUnregister(p);
+        set_error("pipck_host_register: the device address of this range differs from the host address");
+        return PIPCK_EINVAL;
+    }
+    return PIPCK_OK;
+}
+
+int pipck_host_unregister(void* p) {
+    PIPCK_HIP(hipHostUnregister(p));
+    return PIPCK_OK;
+}
+
 void* pipck_host_alloc(size_t bytes) {
+    // coherent (fine-grained): kernels may read it in place (zero-copy TX
+    // segments), and no device cache may keep bytes the host rewrites later
     void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocCoherent) != hipSuccess) return nullptr;
     return p;
 }
 

@@ -1167,6 +1167,19 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
     return PIPCK_OK;
 }
 
+int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
+                     const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo, uint32_t* d_scratch,
+                     uint16_t* d_out, uint32_t* d_err, hipStream_t s) {
+    if (n_segs) {
+        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s);
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_seg_begin,
+                       d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out);
+    PIPCK_LAUNCHED("k_chain_finish");
+    return PIPCK_OK;
+}
+
 }  // namespace pipck
 
 using namespace pipck;
@@ -1249,15 +1262,8 @@ int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_
         set_error("pipck_checksum_chains: null pointer");
         return PIPCK_EINVAL;
     }
-    hipStream_t s = as_stream(stream);
-    if (n_segs) {
-        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s);
-        if (rc) return rc;
-    }
-    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_seg_begin,
-                       d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out);
-    PIPCK_LAUNCHED("k_chain_finish");
-    return PIPCK_OK;
+    return chains_unchecked(d_arena, d_segs, n_segs, d_seg_begin, d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out,
+                            d_err, as_stream(stream));
 }
 
 }  // extern "C"

@@ -90,7 +90,8 @@ struct DevBuf {
 // A queue holds two, so one can be filled while the other is in flight.
 struct TxBatch {
     PinnedBuf bytes;                       // segment bytes, each segment 16-byte aligned
-    std::vector<pipck_desc> inet_segs;     // offsets into `bytes`
+    std::vector<pipck_desc> inet_segs;     // offsets into `bytes`, or (flow == 1) a zero-copy host address
+    bool has_zc = false;                   // some inet segment is read in place from pinned host memory
     std::vector<uint64_t> inet_begin{0};   // CSR: packet p owns inet_segs[begin[p], begin[p+1])
     std::vector<TxPseudo> inet_pseudo;
     std::vector<uint8_t*> inet_field;
@@ -104,6 +105,7 @@ struct TxBatch {
     void clear() {
         bytes.size = 0;
         inet_segs.clear();
+        has_zc = false;
         inet_begin.assign(1, 0);
         inet_pseudo.clear();
         inet_field.clear();
@@ -145,7 +147,7 @@ int append_bytes(TxBatch* b, const void* src, uint32_t len, uint64_t* off) {
     return PIPCK_OK;
 }
 
-int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo& ps, void* field) {
+int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo& ps, void* field, bool zc) {
     if (!q || !field || (nseg && !segs)) {
         set_error("pipck_txq_add: null argument");
         return PIPCK_EINVAL;
@@ -158,6 +160,11 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
     }
     TxBatch* b = &q->batch[q->cur];
     for (uint32_t i = 0; i < nseg; i++) {
+        if (zc) {  // read in place at flush time (pinned host memory, device-accessible at the same address)
+            b->inet_segs.push_back(pipck_desc{(uint64_t)(uintptr_t)segs[i].ptr, segs[i].len, 1u});
+            b->has_zc = true;
+            continue;
+        }
         uint64_t off = 0;
         int rc = append_bytes(b, segs[i].ptr, segs[i].len, &off);
         if (rc) return rc;
@@ -183,18 +190,26 @@ int enqueue(pipck_txq* q, TxBatch* b) {
     const size_t meta_in = o_res, meta_all = al(o_res + (n_in + n_ip) * sizeof(uint16_t));
     int rc = b->meta.reserve(meta_all);
     if (rc) return rc;
+    const size_t nb = al(b->bytes.size);
+    if ((rc = b->d_all.reserve(nb + meta_all))) return rc;
+    uint8_t* d_bytes = (uint8_t*)b->d_all.p;
     uint8_t* m = b->meta.p;
-    if (n_seg) std::memcpy(m + o_segs, b->inet_segs.data(), n_seg * sizeof(pipck_desc));
+    if (b->has_zc) {  // every descriptor becomes an absolute address (arena = null below)
+        pipck_desc* d = reinterpret_cast<pipck_desc*>(m + o_segs);
+        for (uint64_t i = 0; i < n_seg; i++) {
+            const pipck_desc& x = b->inet_segs[i];
+            d[i] = pipck_desc{x.flow ? x.offset : (uint64_t)(uintptr_t)(d_bytes + x.offset), x.len, 0u};
+        }
+    } else if (n_seg) {
+        std::memcpy(m + o_segs, b->inet_segs.data(), n_seg * sizeof(pipck_desc));
+    }
     std::memcpy(m + o_begin, b->inet_begin.data(), (n_in + 1) * sizeof(uint64_t));
     if (n_in) std::memcpy(m + o_rec, b->inet_pseudo.data(), n_in * sizeof(TxPseudo));
     uint32_t* flow = reinterpret_cast<uint32_t*>(m + o_flow);
     for (uint64_t i = 0; i < n_in; i++) flow[i] = (uint32_t)i;  // packet i uses pseudo base i
     if (n_ip) std::memcpy(m + o_ip, b->ip_hdrs.data(), n_ip * sizeof(pipck_desc));
 
-    const size_t nb = al(b->bytes.size);
-    if ((rc = b->d_all.reserve(nb + meta_all))) return rc;
     if ((rc = b->d_work.reserve(al(n_in * 4) + al(std::max<uint64_t>(n_seg, 1) * 4) + 16))) return rc;
-    uint8_t* d_bytes = (uint8_t*)b->d_all.p;
     uint8_t* d_meta = d_bytes + nb;
     uint32_t* d_pseudo = (uint32_t*)b->d_work.p;
     uint32_t* d_scratch = (uint32_t*)((uint8_t*)b->d_work.p + al(n_in * 4));
@@ -206,9 +221,9 @@ int enqueue(pipck_txq* q, TxBatch* b) {
         hipLaunchKernelGGL(k_tx_pseudo, dim3((uint32_t)((n_in + 255) / 256)), dim3(256), 0, s,
                            (const TxPseudo*)(d_meta + o_rec), (uint32_t)n_in, d_pseudo);
         PIPCK_LAUNCHED("k_tx_pseudo");
-        rc = pipck_checksum_chains(d_bytes, (const pipck_desc*)(d_meta + o_segs), n_seg,
-                                   (const uint64_t*)(d_meta + o_begin), (const uint32_t*)(d_meta + o_flow), n_in,
-                                   d_pseudo, d_scratch, d_res, nullptr, s);
+        rc = chains_unchecked(b->has_zc ? nullptr : d_bytes, (const pipck_desc*)(d_meta + o_segs), n_seg,
+                              (const uint64_t*)(d_meta + o_begin), (const uint32_t*)(d_meta + o_flow), n_in, d_pseudo,
+                              d_scratch, d_res, nullptr, s);
         if (rc) return rc;
     }
     if (n_ip) {
@@ -292,7 +307,17 @@ int pipck_txq_add4(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t 
     ps.proto = proto;
     std::memcpy(ps.src, &src, 4);
     std::memcpy(ps.dst, &dst, 4);
-    return add_inet(q, segs, nseg, ps, csum_field);
+    return add_inet(q, segs, nseg, ps, csum_field, false);
+}
+
+int pipck_txq_add4_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, uint32_t src,
+                      uint32_t dst, void* csum_field) {
+    TxPseudo ps{};
+    ps.family = 4;
+    ps.proto = proto;
+    std::memcpy(ps.src, &src, 4);
+    std::memcpy(ps.dst, &dst, 4);
+    return add_inet(q, segs, nseg, ps, csum_field, true);
 }
 
 int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
@@ -306,7 +331,21 @@ int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t 
     ps.proto = proto;
     std::memcpy(ps.src, src, 16);
     std::memcpy(ps.dst, dst, 16);
-    return add_inet(q, segs, nseg, ps, csum_field);
+    return add_inet(q, segs, nseg, ps, csum_field, false);
+}
+
+int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
+                      const uint8_t* dst, void* csum_field) {
+    if (!src || !dst) {
+        set_error("pipck_txq_add6_zc: null address");
+        return PIPCK_EINVAL;
+    }
+    TxPseudo ps{};
+    ps.family = 6;
+    ps.proto = proto;
+    std::memcpy(ps.src, src, 16);
+    std::memcpy(ps.dst, dst, 16);
+    return add_inet(q, segs, nseg, ps, csum_field, true);
 }
 
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field) {

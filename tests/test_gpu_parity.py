@@ -772,3 +772,79 @@ def test_txq_submit_complete_pipeline(oracle):
     finally:
         lib.pipck_txq_destroy(q)
         lib.pipck_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_txq_zero_copy_segments(oracle, register):
+    """pipck_txq_add4_zc / add6_zc: segments read in place from pinned host
+    memory (pipck_host_alloc, or a registered numpy buffer), mixed in one batch
+    with staged chains and IPv4 headers; flushed and pipelined."""
+    lib = _lib.load()
+    ctx, q = C.c_void_p(), C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    rng = np.random.default_rng(4321 + register)
+    size = 4 << 20
+    if register:
+        host = np.zeros(size + 4096, dtype=np.uint8)
+        off0 = (-host.ctypes.data) % 4096
+        pool = host[off0:off0 + size]
+        base = pool.ctypes.data
+        _lib.check("pipck_host_register", lib.pipck_host_register(C.c_void_p(base), size))
+    else:
+        base = lib.pipck_host_alloc(size)
+        assert base
+        pool = np.ctypeslib.as_array((C.c_uint8 * size).from_address(base))
+    try:
+        for rnd in range(2):
+            n_pk = 700
+            fields = (C.c_uint8 * (2 * n_pk))()
+            keep, want, pos = [], [], 0
+            for i in range(n_pk):
+                field = C.c_void_p(C.addressof(fields) + 2 * i)
+                kind = int(rng.integers(0, 4))
+                segs = [rng.integers(0, 256, int(rng.choice([20, 32, rng.integers(0, 9), rng.integers(0, 3000)])),
+                                     dtype=np.uint8).tobytes() for _ in range(int(rng.integers(1, 4)))]
+                if kind == 3:  # IPv4 header (staged)
+                    hdr = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+                    hdr[10:12] = b"\0\0"
+                    b = C.create_string_buffer(bytes(hdr), 20)
+                    keep.append(b)
+                    _lib.check("add_ip", lib.pipck_txq_add_ip(q, b, 20, field))
+                    want.append(oracle.ip_checksum(bytes(hdr)))
+                    continue
+                arr = (_lib.HSeg * len(segs))()
+                for j, sgm in enumerate(segs):
+                    if kind in (0, 1):  # zero-copy: bytes placed in the pinned pool at any alignment
+                        pos += int(rng.integers(0, 16))
+                        pool[pos:pos + len(sgm)] = np.frombuffer(sgm, dtype=np.uint8)
+                        arr[j].ptr = C.c_void_p(base + pos)
+                        pos += len(sgm)
+                    else:
+                        b = C.create_string_buffer(sgm, max(len(sgm), 1))
+                        keep.append(b)
+                        arr[j].ptr = C.cast(b, C.c_void_p)
+                    arr[j].len = len(sgm)
+                proto = int(rng.choice([6, 17]))
+                if kind in (0, 2):
+                    s, d = rng.bytes(4), rng.bytes(4)
+                    fn = lib.pipck_txq_add4_zc if kind == 0 else lib.pipck_txq_add4
+                    _lib.check("add4", fn(q, arr, len(segs), proto, int.from_bytes(s, "little"),
+                                          int.from_bytes(d, "little"), field))
+                    want.append(oracle.inet_checksum_chain(segs, proto, s, d))
+                else:
+                    s, d = rng.bytes(16), rng.bytes(16)
+                    _lib.check("add6_zc", lib.pipck_txq_add6_zc(q, arr, len(segs), proto, s, d, field))
+                    want.append(oracle.inet6_checksum_chain(segs, proto, s, d))
+                if rnd == 1 and i % 100 == 99:
+                    _lib.check("submit", lib.pipck_txq_submit(q))
+            _lib.check("flush", lib.pipck_txq_flush(q))
+            got = np.frombuffer(bytes(fields), dtype=">u2")
+            assert np.array_equal(got, np.array(want, dtype=np.uint16)), (rnd, np.nonzero(got != want)[0][:5])
+    finally:
+        lib.pipck_txq_destroy(q)
+        lib.pipck_ctx_destroy(ctx)
+        if register:
+            lib.pipck_host_unregister(C.c_void_p(base))
+        else:
+            lib.pipck_host_free(C.c_void_p(base))

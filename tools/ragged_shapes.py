@@ -26,7 +26,8 @@ from size_scan import timed  # noqa: E402
 
 SHAPES = [("uniform_8980", 8980, 2 << 20), ("uniform_1480", 1480, 8 << 20), ("uniform_512", 512, 16 << 20),
           ("uniform_128", 128, 32 << 20), ("uniform_64", 64, 64 << 20), ("uniform_40", 40, 64 << 20),
-          ("uniform_20", 20, 128 << 20), ("zipf_cfg4", 0, 8 << 20), ("zipf_cfg4_32M", 0, 32 << 20)]
+          ("uniform_20", 20, 128 << 20), ("zipf_cfg4", 0, 8 << 20), ("zipf_cfg4_32M", 0, 32 << 20),
+          ("zipf_plus192", -192, 8 << 20), ("zipf_plus448", -448, 8 << 20), ("zipf_plus960", -960, 8 << 20)]
 
 
 def main():
@@ -60,7 +61,14 @@ def main():
     for name, length, n in SHAPES:
         if a.only and name not in a.only.split(","):
             continue
-        lengths = None if length == 0 else torch.full((n,), length, dtype=torch.int32, device="cuda")
+        if length > 0:
+            lengths = torch.full((n,), length, dtype=torch.int32, device="cuda")
+        elif length < 0:  # cfg4's Zipf lengths shifted up by -length bytes (capped at 9000)
+            z = torch.empty(n, dtype=torch.int32, device="cuda")
+            engine.call("pipck_gen_zipf_lengths", engine._ptr(z), n, 0, w.seed, engine.current_stream())
+            lengths = torch.clamp(z - length, max=9000)
+        else:
+            lengths = None
         arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS, lengths=lengths)
         nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
         arms = {"ragged": lambda: engine.checksum_ragged(arena, desc, pseudo)}
@@ -72,7 +80,7 @@ def main():
                 finally:
                     engine.tune()
             arms["ragged_no_tiny"] = ragged_stream
-        if length:
+        if length > 0:
             stride = (length + 15) // 16 * 16
 
             def fixed(**kw):

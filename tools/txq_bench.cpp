@@ -6,11 +6,14 @@
 // does (a 20-byte header segment with th_sum = 0 chained to a payload
 // segment, pip/protocol/pip_tcp_packet.cpp:28-37) and checksums them through
 // TX queues, `threads` producer threads with one queue each over their share
-// of the packets.  Two modes, each timed over `rounds` repetitions (best kept):
+// of the packets.  Three modes, each timed over `rounds` repetitions (best kept):
 //   sync       add every packet, then pipck_txq_flush (one H2D, one GPU batch,
 //              one D2H, htons(result) into every header);
 //   pipelined  add `batch` packets, pipck_txq_submit, add the next `batch`
-//              while the previous one is in flight; pipck_txq_complete at the end.
+//              while the previous one is in flight; pipck_txq_complete at the end;
+//   zero_copy  pipelined, with headers and payloads in pinned host memory
+//              (pipck_host_alloc) added by pipck_txq_add4_zc: the GPU reads
+//              them in place, nothing is copied at add time.
 // Every header's th_sum is checked against the first sync round.  Prints one
 // JSON line per mode: host-to-host rate of the whole add+flush cycle.
 #include <algorithm>
@@ -31,16 +34,15 @@ struct Shard {
     int rc = 0;
 };
 
-int add_packet(pipck_txq* q, std::vector<uint8_t>& hdr, const std::vector<uint8_t>& body, uint32_t payload,
-               uint32_t i) {
+int add_packet(pipck_txq* q, uint8_t* hdr, const uint8_t* body, uint32_t payload, uint32_t i, bool zc) {
     pipck_hseg segs[2] = {{&hdr[(size_t)i * 20], 20}, {&body[(size_t)i * payload], payload}};
-    return pipck_txq_add4(q, segs, 2, 6, 0x0100000Au + (i & 1023), 0x0200000Au, &hdr[(size_t)i * 20 + 16]);
+    return (zc ? pipck_txq_add4_zc : pipck_txq_add4)(q, segs, 2, 6, 0x0100000Au + (i & 1023), 0x0200000Au,
+                                                      &hdr[(size_t)i * 20 + 16]);
 }
 
-int run_shard(Shard& s, std::vector<uint8_t>& hdr, const std::vector<uint8_t>& body, uint32_t payload, bool pipelined,
-              uint32_t batch) {
+int run_shard(Shard& s, uint8_t* hdr, const uint8_t* body, uint32_t payload, bool pipelined, uint32_t batch, bool zc) {
     for (uint32_t i = s.first; i < s.first + s.n; i++) {
-        int rc = add_packet(s.q, hdr, body, payload, i);
+        int rc = add_packet(s.q, hdr, body, payload, i, zc);
         if (rc) return rc;
         if (pipelined && (i - s.first + 1) % batch == 0 && (rc = pipck_txq_submit(s.q))) return rc;
     }
@@ -59,9 +61,16 @@ int main(int argc, char** argv) {
     const int rounds = argc > 3 ? atoi(argv[3]) : 5;
     const uint32_t threads = std::max(1, argc > 4 ? atoi(argv[4]) : 1);
     const uint32_t batch = std::max(1, argc > 5 ? atoi(argv[5]) : 16384);
-    std::vector<uint8_t> hdr((size_t)n * 20), body((size_t)n * payload);
-    for (size_t i = 0; i < body.size(); i++) body[i] = (uint8_t)(i * 2654435761u >> 24);
-    for (size_t i = 0; i < hdr.size(); i++) hdr[i] = (uint8_t)(i * 40503u >> 8);
+    // pinned, so the zero-copy mode can read them in place (the copying modes do not care)
+    const size_t hdr_n = (size_t)n * 20, body_n = (size_t)n * payload;
+    uint8_t* hdr = (uint8_t*)pipck_host_alloc(hdr_n);
+    uint8_t* body = (uint8_t*)pipck_host_alloc(body_n ? body_n : 1);
+    if (!hdr || !body) {
+        fprintf(stderr, "txq_bench: pinned allocation failed\n");
+        return 1;
+    }
+    for (size_t i = 0; i < body_n; i++) body[i] = (uint8_t)(i * 2654435761u >> 24);
+    for (size_t i = 0; i < hdr_n; i++) hdr[i] = (uint8_t)(i * 40503u >> 8);
     pipck_ctx* ctx = nullptr;
     if (pipck_ctx_create(-1, &ctx)) {
         fprintf(stderr, "txq_bench: %s\n", pipck_last_error());
@@ -77,15 +86,16 @@ int main(int argc, char** argv) {
         }
     }
     std::vector<uint8_t> want;  // th_sum of every packet from the first sync round
-    for (int mode = 0; mode < 2; mode++) {
-        const bool pipelined = mode == 1;
+    static const char* kModes[] = {"sync", "pipelined", "zero_copy"};
+    for (int mode = 0; mode < 3; mode++) {
+        const bool pipelined = mode >= 1, zc = mode == 2;
         double best = 1e30;
         for (int r = 0; r < rounds; r++) {
             for (uint32_t i = 0; i < n; i++) hdr[(size_t)i * 20 + 16] = hdr[(size_t)i * 20 + 17] = 0;
             auto t0 = std::chrono::steady_clock::now();
             std::vector<std::thread> th;
             for (auto& s : shards)
-                th.emplace_back([&, pipelined] { s.rc = run_shard(s, hdr, body, payload, pipelined, batch); });
+                th.emplace_back([&, pipelined, zc] { s.rc = run_shard(s, hdr, body, payload, pipelined, batch, zc); });
             for (auto& x : th) x.join();
             auto t1 = std::chrono::steady_clock::now();
             for (auto& s : shards) {
@@ -100,19 +110,20 @@ int main(int argc, char** argv) {
             if (want.empty()) {
                 want = got;
             } else if (got != want) {
-                fprintf(stderr, "txq_bench: %s round %d: checksums differ from the first round\n",
-                        pipelined ? "pipelined" : "sync", r);
+                fprintf(stderr, "txq_bench: %s round %d: checksums differ from the first round\n", kModes[mode], r);
                 return 1;
             }
         }
         const double bytes = (double)n * (20 + payload);
         printf("{\"tool\": \"txq_bench\", \"mode\": \"%s\", \"threads\": %u, \"batch\": %u, \"packets\": %u, "
                "\"l4_bytes\": %u, \"gib_per_s\": %.2f, \"mpkt_per_s\": %.3f, \"ms\": %.2f}\n",
-               pipelined ? "pipelined" : "sync", threads, pipelined ? batch : n, n, 20 + payload,
+               kModes[mode], threads, pipelined ? batch : n, n, 20 + payload,
                bytes / best / (1u << 30), n / best / 1e6, best * 1e3);
         fflush(stdout);
     }
     for (auto& s : shards) pipck_txq_destroy(s.q);
     pipck_ctx_destroy(ctx);
+    pipck_host_free(hdr);
+    pipck_host_free(body);
     return 0;
 }
