@@ -237,7 +237,9 @@ int pipck_txq_add6(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t 
 /* Zero-copy forms: the segments lie in pinned host memory (pipck_host_alloc or
  * pipck_host_register) and are read by the GPU in place when the batch runs --
  * nothing is copied at add time, so they must stay valid and unchanged until
- * the batch completes (flush, or the complete/submit after its submit). */
+ * the batch completes (flush, or the complete/submit after its submit).  A
+ * segment outside every such range is refused (PIPCK_EINVAL): the GPU must
+ * never touch an unpinned host page. */
 int pipck_txq_add4_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, uint32_t src,
                       uint32_t dst, void* csum_field);
 int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,

@@ -35,6 +35,18 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // Number of CUs on the current device (cached per device).
 int device_cus();
 
+// Registry of the pinned host ranges the GPU may read in place (made by
+// pipck_host_alloc / pipck_host_register).  Zero-copy TX segments are checked
+// against it at add time: a kernel touching an unpinned host page would fault
+// the GPU, so a bad pointer must fail as PIPCK_EINVAL instead.
+struct PinnedRange {
+    uintptr_t lo = 0, hi = 0;  // [lo, hi)
+};
+void pinned_add(const void* p, size_t bytes);
+void pinned_remove(const void* p);
+// true if [p, p+len) lies inside one registered range; *hit returns that range
+bool pinned_lookup(const void* p, size_t len, PinnedRange* hit);
+
 // pipck_checksum_chains without argument checks, for callers whose segment
 // descriptors hold absolute device-accessible addresses (d_arena == nullptr):
 // the TX queue mixes its device staging copy with zero-copy pinned host segments.

@@ -14,7 +14,9 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -30,6 +32,30 @@ static std::atomic<int> g_zero_copy{[] {
 }()};
 constexpr size_t kZeroCopyMax = 64u << 10;
 void set_error(const std::string& msg) { t_err = msg; }
+
+static std::shared_mutex g_pinned_mu;
+static std::map<uintptr_t, uintptr_t> g_pinned;  // lo -> hi
+
+void pinned_add(const void* p, size_t bytes) {
+    std::unique_lock<std::shared_mutex> g(g_pinned_mu);
+    g_pinned[(uintptr_t)p] = (uintptr_t)p + bytes;
+}
+
+void pinned_remove(const void* p) {
+    std::unique_lock<std::shared_mutex> g(g_pinned_mu);
+    g_pinned.erase((uintptr_t)p);
+}
+
+bool pinned_lookup(const void* p, size_t len, PinnedRange* hit) {
+    const uintptr_t a = (uintptr_t)p;
+    std::shared_lock<std::shared_mutex> g(g_pinned_mu);
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return false;
+    --it;
+    if (a + len > it->second) return false;
+    if (hit) *hit = PinnedRange{it->first, it->second};
+    return true;
+}
 
 int device_cus() {
     static std::mutex mu;
@@ -274,10 +300,12 @@ int pipck_host_register(void* p, size_t bytes) {
         set_error("pipck_host_register: the device address of this range differs from the host address");
         return PIPCK_EINVAL;
     }
+    pinned_add(p, bytes);
     return PIPCK_OK;
 }
 
 int pipck_host_unregister(void* p) {
+    pinned_remove(p);
     PIPCK_HIP(hipHostUnregister(p));
     return PIPCK_OK;
 }
@@ -287,11 +315,14 @@ void* pipck_host_alloc(size_t bytes) {
     // segments), and no device cache may keep bytes the host rewrites later
     void* p = nullptr;
     if (hipHostMalloc(&p, bytes, hipHostMallocCoherent) != hipSuccess) return nullptr;
+    pinned_add(p, bytes);
     return p;
 }
 
 void pipck_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    pinned_remove(p);
+    (void)hipHostFree(p);
 }
 
 int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride, uint32_t len, uint64_t n,

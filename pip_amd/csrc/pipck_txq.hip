@@ -130,6 +130,8 @@ struct pipck_txq {
     hipEvent_t done = nullptr;  // recorded after the in-flight batch's D2H copy
     int device = 0;
     TxBatch batch[2];
+    PinnedRange pin_cache[4];  // pinned ranges of recent zero-copy segments (headers and payloads
+    unsigned pin_next = 0;     // usually come from a few buffers): most checks skip the registry
     int cur = 0;         // batch receiving adds
     bool inflight = false;  // batch[cur ^ 1] has been submitted and not completed
 };
@@ -156,6 +158,20 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
         if (segs[i].len > PIPCK_MAX_SEG_LEN || (segs[i].len && !segs[i].ptr)) {
             set_error("pipck_txq_add: segment null or longer than 65535 bytes");
             return PIPCK_ERANGE;
+        }
+        if (zc && segs[i].len) {  // the GPU will read it in place: it must be pinned
+            const uintptr_t a = (uintptr_t)segs[i].ptr;
+            bool ok = false;
+            for (const PinnedRange& r : q->pin_cache) ok |= a >= r.lo && a + segs[i].len <= r.hi;
+            if (!ok) {
+                PinnedRange r;
+                if (!pinned_lookup(segs[i].ptr, segs[i].len, &r)) {
+                    set_error("pipck_txq_add_zc: segment outside every range from pipck_host_alloc / "
+                              "pipck_host_register");
+                    return PIPCK_EINVAL;
+                }
+                q->pin_cache[q->pin_next++ % 4] = r;
+            }
         }
     }
     TxBatch* b = &q->batch[q->cur];

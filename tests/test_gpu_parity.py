@@ -796,6 +796,15 @@ def test_txq_zero_copy_segments(oracle, register):
         assert base
         pool = np.ctypeslib.as_array((C.c_uint8 * size).from_address(base))
     try:
+        # a segment outside every pinned range is refused, and nothing is queued
+        plain = C.create_string_buffer(b"x" * 64, 64)
+        bad = (_lib.HSeg * 1)()
+        bad[0].ptr, bad[0].len = C.cast(plain, C.c_void_p), 64
+        fld = (C.c_uint8 * 2)()
+        assert lib.pipck_txq_add4_zc(q, bad, 1, 6, 1, 2, C.cast(fld, C.c_void_p)) == _lib.PIPCK_EINVAL
+        bad[0].ptr, bad[0].len = C.c_void_p(base + size - 8), 64  # runs past the end of the range
+        assert lib.pipck_txq_add4_zc(q, bad, 1, 6, 1, 2, C.cast(fld, C.c_void_p)) == _lib.PIPCK_EINVAL
+        assert lib.pipck_txq_pending(q) == 0
         for rnd in range(2):
             n_pk = 700
             fields = (C.c_uint8 * (2 * n_pk))()
