@@ -13,6 +13,7 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -43,7 +44,8 @@ __global__ void k_tx_pseudo(const TxPseudo* __restrict__ rec, uint32_t n, uint32
     pseudo[i] = s;
 }
 
-// A growable pinned host buffer.
+// A growable pinned host buffer; coherent, so small flushes can let the kernels
+// read it (and write results into it) in place.
 struct PinnedBuf {
     uint8_t* p = nullptr;
     size_t size = 0, cap = 0;
@@ -52,7 +54,7 @@ struct PinnedBuf {
         size_t nc = cap ? cap : (1u << 20);
         while (nc < need) nc *= 2;
         uint8_t* np = nullptr;
-        PIPCK_HIP(hipHostMalloc((void**)&np, nc, hipHostMallocDefault));
+        PIPCK_HIP(hipHostMalloc((void**)&np, nc, hipHostMallocCoherent));
         if (size) std::memcpy(np, p, size);
         if (p) (void)hipHostFree(p);
         p = np;
@@ -192,8 +194,23 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
     return PIPCK_OK;
 }
 
-// Enqueue batch b on the queue's stream: H2D of bytes + metadata, the
-// pseudo-header and chain kernels, ragged IPv4 headers, D2H of the results.
+// A flush whose staged bytes + metadata fit 32 MiB runs without any copy
+// command: the kernels read the coherent pinned staging in place and write the
+// results into it.  Measured on one producer thread (tools/txq_bench.cpp,
+// profiles/r01_txq_inplace_ab.jsonl): a 64-packet flush 40 vs 50 us, 1,024
+// packets 0.10 vs 0.12 ms, pipelined 16K-packet batches +15 %.  Larger batches
+// keep the H2D / D2H copies.
+static size_t in_place_flush_max() {
+    static const size_t v = [] {
+        const char* e = getenv("PIPCK_TXQ_INPLACE_MAX");  // bytes; 0 disables (tools/txq_bench A/B)
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(32u << 20);
+    }();
+    return v;
+}
+
+// Enqueue batch b on the queue's stream: H2D of bytes + metadata (or nothing,
+// for a small batch), the pseudo-header and chain kernels, ragged IPv4
+// headers, D2H of the results (or results written in place).
 int enqueue(pipck_txq* q, TxBatch* b) {
     const uint64_t n_in = b->inet_field.size(), n_ip = b->ip_field.size(), n_seg = b->inet_segs.size();
     // meta layout (each part 16-byte aligned): inet segs | inet begin | pseudo recs | flow ids | ip descs | results
@@ -207,8 +224,15 @@ int enqueue(pipck_txq* q, TxBatch* b) {
     int rc = b->meta.reserve(meta_all);
     if (rc) return rc;
     const size_t nb = al(b->bytes.size);
-    if ((rc = b->d_all.reserve(nb + meta_all))) return rc;
-    uint8_t* d_bytes = (uint8_t*)b->d_all.p;
+    const bool in_place = nb + meta_all <= in_place_flush_max();
+    uint8_t* d_bytes = nullptr;
+    if (in_place) {
+        if ((rc = b->bytes.reserve(16))) return rc;  // a valid base even for an empty batch
+        d_bytes = b->bytes.p;
+    } else {
+        if ((rc = b->d_all.reserve(nb + meta_all))) return rc;
+        d_bytes = (uint8_t*)b->d_all.p;
+    }
     uint8_t* m = b->meta.p;
     if (b->has_zc) {  // every descriptor becomes an absolute address (arena = null below)
         pipck_desc* d = reinterpret_cast<pipck_desc*>(m + o_segs);
@@ -226,12 +250,14 @@ int enqueue(pipck_txq* q, TxBatch* b) {
     if (n_ip) std::memcpy(m + o_ip, b->ip_hdrs.data(), n_ip * sizeof(pipck_desc));
 
     if ((rc = b->d_work.reserve(al(n_in * 4) + al(std::max<uint64_t>(n_seg, 1) * 4) + 16))) return rc;
-    uint8_t* d_meta = d_bytes + nb;
+    uint8_t* d_meta = in_place ? m : d_bytes + nb;
     uint32_t* d_pseudo = (uint32_t*)b->d_work.p;
     uint32_t* d_scratch = (uint32_t*)((uint8_t*)b->d_work.p + al(n_in * 4));
     hipStream_t s = q->stream;
-    if (b->bytes.size) PIPCK_HIP(hipMemcpyAsync(d_bytes, b->bytes.p, b->bytes.size, hipMemcpyHostToDevice, s));
-    PIPCK_HIP(hipMemcpyAsync(d_meta, m, meta_in, hipMemcpyHostToDevice, s));
+    if (!in_place) {
+        if (b->bytes.size) PIPCK_HIP(hipMemcpyAsync(d_bytes, b->bytes.p, b->bytes.size, hipMemcpyHostToDevice, s));
+        PIPCK_HIP(hipMemcpyAsync(d_meta, m, meta_in, hipMemcpyHostToDevice, s));
+    }
     uint16_t* d_res = (uint16_t*)(d_meta + o_res);
     if (n_in) {
         hipLaunchKernelGGL(k_tx_pseudo, dim3((uint32_t)((n_in + 255) / 256)), dim3(256), 0, s,
@@ -246,7 +272,8 @@ int enqueue(pipck_txq* q, TxBatch* b) {
         rc = pipck_checksum_ragged(d_bytes, (const pipck_desc*)(d_meta + o_ip), n_ip, nullptr, d_res + n_in, nullptr, s);
         if (rc) return rc;
     }
-    PIPCK_HIP(hipMemcpyAsync(m + o_res, d_res, (n_in + n_ip) * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+    if (!in_place)
+        PIPCK_HIP(hipMemcpyAsync(m + o_res, d_res, (n_in + n_ip) * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
     PIPCK_HIP(hipEventRecord(q->done, s));
     b->o_res = o_res;
     return PIPCK_OK;

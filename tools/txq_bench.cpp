@@ -93,10 +93,14 @@ int main(int argc, char** argv) {
         for (int r = 0; r < rounds; r++) {
             for (uint32_t i = 0; i < n; i++) hdr[(size_t)i * 20 + 16] = hdr[(size_t)i * 20 + 17] = 0;
             auto t0 = std::chrono::steady_clock::now();
-            std::vector<std::thread> th;
-            for (auto& s : shards)
-                th.emplace_back([&, pipelined, zc] { s.rc = run_shard(s, hdr, body, payload, pipelined, batch, zc); });
-            for (auto& x : th) x.join();
+            if (threads == 1) {  // inline: a thread spawn would dominate small batches
+                shards[0].rc = run_shard(shards[0], hdr, body, payload, pipelined, batch, zc);
+            } else {
+                std::vector<std::thread> th;
+                for (auto& s : shards)
+                    th.emplace_back([&, pipelined, zc] { s.rc = run_shard(s, hdr, body, payload, pipelined, batch, zc); });
+                for (auto& x : th) x.join();
+            }
             auto t1 = std::chrono::steady_clock::now();
             for (auto& s : shards) {
                 if (s.rc) {
