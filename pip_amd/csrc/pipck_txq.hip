@@ -200,12 +200,9 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
 // profiles/r01_txq_inplace_ab.jsonl): a 64-packet flush 40 vs 50 us, 1,024
 // packets 0.10 vs 0.12 ms, pipelined 16K-packet batches +15 %.  Larger batches
 // keep the H2D / D2H copies.
-static size_t in_place_flush_max() {
-    static const size_t v = [] {
-        const char* e = getenv("PIPCK_TXQ_INPLACE_MAX");  // bytes; 0 disables (tools/txq_bench A/B)
-        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(32u << 20);
-    }();
-    return v;
+static size_t in_place_flush_max() {  // read per flush: tests and A/Bs switch it at run time
+    const char* e = getenv("PIPCK_TXQ_INPLACE_MAX");  // bytes; 0 = always copy
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(32u << 20);
 }
 
 // Enqueue batch b on the queue's stream: H2D of bytes + metadata (or nothing,

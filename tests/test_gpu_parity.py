@@ -675,7 +675,12 @@ def test_full_size_ragged(oracle):
 # ----------------------------------------------------------------------------
 # 9. deferred TX queue: mixed v4/v6 chains + IPv4 headers
 # ----------------------------------------------------------------------------
-def test_txq_mixed_batches_vs_oracle(oracle):
+@pytest.mark.parametrize("in_place", [True, False])
+def test_txq_mixed_batches_vs_oracle(oracle, in_place, monkeypatch):
+    """in_place: small flushes read the pinned staging in place (default);
+    False forces the H2D / D2H copy path that large flushes take."""
+    if not in_place:
+        monkeypatch.setenv("PIPCK_TXQ_INPLACE_MAX", "0")
     lib = _lib.load()
     ctx, q = C.c_void_p(), C.c_void_p()
     _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
@@ -774,11 +779,14 @@ def test_txq_submit_complete_pipeline(oracle):
         lib.pipck_ctx_destroy(ctx)
 
 
+@pytest.mark.parametrize("in_place", [True, False])
 @pytest.mark.parametrize("register", [False, True])
-def test_txq_zero_copy_segments(oracle, register):
+def test_txq_zero_copy_segments(oracle, register, in_place, monkeypatch):
     """pipck_txq_add4_zc / add6_zc: segments read in place from pinned host
     memory (pipck_host_alloc, or a registered numpy buffer), mixed in one batch
     with staged chains and IPv4 headers; flushed and pipelined."""
+    if not in_place:
+        monkeypatch.setenv("PIPCK_TXQ_INPLACE_MAX", "0")
     lib = _lib.load()
     ctx, q = C.c_void_p(), C.c_void_p()
     _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
