@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# GPU box: parity tests, then a same-process A/B of the current build against
+# GPU box: parity tests, then an A/B (each build in its own process) of the current build against
 # the libraries named in $AB (default pip_amd/lib/ab/*.so).  Stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
