@@ -12,6 +12,7 @@
 #include "pipck_device.hpp"
 
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -124,7 +125,10 @@ __global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict_
         __syncthreads();
     }
     // pip's chain always holds at least one pip_buf: zero segments == one empty segment
-    if (threadIdx.x == 0) *out = nseg ? sum : fold16(sum);
+    // a system-scope release: the zero-copy caller spins on this word in host
+    // memory instead of synchronising the stream (all reads of the staging
+    // buffer are done by now)
+    if (threadIdx.x == 0) __hip_atomic_store(out, nseg ? sum : fold16(sum), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace pipck
@@ -270,10 +274,25 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
     if (zc == 1 || (zc == 2 && need <= kZeroCopyMax)) {
         // The kernel reads the pinned staging buffer over PCIe and writes the
         // result into pinned host memory: no copy commands around the launch.
-        *c->h_result = 0xFFFFFFFFu;
+        // The result (<= 0xFFFF) replaces a sentinel no sum can take; the host
+        // spins on it rather than synchronising the stream, and falls back to
+        // a synchronise (which also reports a failed kernel) after 2 ms.
+        __atomic_store_n(c->h_result, 0xFFFFFFFFu, __ATOMIC_RELAXED);
         hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->h_stage + table,
                            reinterpret_cast<const SegRef*>(c->h_stage), nseg, init, c->h_result);
         PIPCK_LAUNCHED("k_exact_chain");
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t v;
+        while ((v = __atomic_load_n(c->h_result, __ATOMIC_ACQUIRE)) == 0xFFFFFFFFu) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+                PIPCK_HIP(hipStreamSynchronize(s));
+                v = __atomic_load_n(c->h_result, __ATOMIC_ACQUIRE);
+                break;
+            }
+            __builtin_ia32_pause();
+        }
+        *out = v;
+        return PIPCK_OK;
     } else {
         if (need) PIPCK_HIP(hipMemcpyAsync(c->d_stage, c->h_stage, need, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_exact_chain, dim3(1), dim3(1024), 0, s, c->d_stage + table,
