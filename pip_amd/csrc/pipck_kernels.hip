@@ -384,7 +384,7 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
 }
 
 template <int U>
-constexpr int flat_waves_per_simd() { return U >= 16 ? 4 : (U >= 8 ? 5 : 6); }
+constexpr int flat_waves_per_simd() { return U >= 32 ? 2 : (U >= 16 ? 4 : (U >= 8 ? 5 : 6)); }
 
 template <int U, bool PIPE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
@@ -978,10 +978,10 @@ struct FlatVariant {
             {k_flat<U, P, true, false>, k_flat<U, P, true, true>}                         \
         }                                                                                 \
     }
-// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9 = pipelined U = 2/4/8
+// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/33 = ring-pipelined U = 2/4/8/12/16/32
 static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_F(8, false), PIPCK_F(16, false),
                                     PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
-                                    PIPCK_F(16, true)};
+                                    PIPCK_F(16, true), PIPCK_F(32, true)};
 #undef PIPCK_F
 static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
     {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
@@ -998,6 +998,7 @@ static const FlatVariant& flat_variant(uint32_t loads) {
         case 16: return kFlat[3];
         case 13: return kFlat[7];
         case 17: return kFlat[8];
+        case 33: return kFlat[9];
         default: return kFlat[2];
     }
 }
@@ -1050,15 +1051,18 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        // rows in flight per wave: a ring of 16 (cfg2: 0-5 % over 8 plain rows,
-        // profiles/r01_size_scan12_cfg2_cfg3.jsonl; ring vs plain 16: cfg2 +1 %,
-        // cfg3 +0.5 %, cfg5 even, profiles/r01_flat_ring_scan.jsonl)
-        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : 17u;
+        // Rows in flight per wave and task size.  Jumbo packets (>= 4 KiB, cfg3
+        // and cfg5): a ring of 32 rows (191 VGPRs, 2 waves/SIMD) over ~128-row
+        // tasks, +1.9 % on cfg5 (7.12 TB/s) and +3.5 % on cfg3 over a ring of 16
+        // with 64-row tasks (profiles/r01_flat_deep_ring_scan.jsonl).  Shorter
+        // packets: a ring of 16 over ~64-row tasks (the deep ring cost cfg2
+        // 8 %; ring 16 vs 8 plain rows +0-5 %, r01_size_scan12_cfg2_cfg3.jsonl,
+        // r01_flat_ring_scan.jsonl).  One task per wave either way.
+        const bool jumbo = cpp >= 256;
+        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (jumbo ? 33u : 17u);
         const FlatVariant* fv = &flat_variant(loads);
-        // a wave task covers ~64 rows of 1 KiB and the grid holds one task per wave
-        // (measured best for 1.5-9 KiB packets at 19-150 GB, profiles/r01_size_scan3.jsonl)
         const uint32_t flags = g_tune.flags.load();
-        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 64u;
+        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 128u : 64u);
         const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
