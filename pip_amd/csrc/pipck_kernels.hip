@@ -384,7 +384,7 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
 }
 
 template <int U>
-constexpr int flat_waves_per_simd() { return U >= 32 ? 2 : (U >= 16 ? 4 : (U >= 8 ? 5 : 6)); }
+constexpr int flat_waves_per_simd() { return U >= 32 ? 2 : (U >= 24 ? 3 : (U >= 16 ? 4 : (U >= 8 ? 5 : 6))); }
 
 template <int U, bool PIPE, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
@@ -978,10 +978,10 @@ struct FlatVariant {
             {k_flat<U, P, true, false>, k_flat<U, P, true, true>}                         \
         }                                                                                 \
     }
-// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/33 = ring-pipelined U = 2/4/8/12/16/32
+// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/25/33/41 = ring-pipelined U = 2/4/8/12/16/24/32/40
 static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_F(8, false), PIPCK_F(16, false),
                                     PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
-                                    PIPCK_F(16, true), PIPCK_F(32, true)};
+                                    PIPCK_F(16, true), PIPCK_F(32, true), PIPCK_F(24, true), PIPCK_F(40, true)};
 #undef PIPCK_F
 static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
     {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
@@ -999,6 +999,8 @@ static const FlatVariant& flat_variant(uint32_t loads) {
         case 13: return kFlat[7];
         case 17: return kFlat[8];
         case 33: return kFlat[9];
+        case 25: return kFlat[10];
+        case 41: return kFlat[11];
         default: return kFlat[2];
     }
 }
@@ -1055,11 +1057,10 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // and cfg5): a ring of 32 rows (191 VGPRs, 2 waves/SIMD) over ~128-row
         // tasks, +1.9 % on cfg5 (7.12 TB/s) and +3.5 % on cfg3 over a ring of 16
         // with 64-row tasks (profiles/r01_flat_deep_ring_scan.jsonl).  Shorter
-        // packets: a ring of 16 over ~64-row tasks (the deep ring cost cfg2
-        // 8 %; ring 16 vs 8 plain rows +0-5 %, r01_size_scan12_cfg2_cfg3.jsonl,
-        // r01_flat_ring_scan.jsonl).  One task per wave either way.
+        // packets: a ring of 24 over ~64-row tasks (cfg2 +0.7-1.4 % over 16 in
+        // three scans; a ring of 32 cost it 8-15 %).  One task per wave either way.
         const bool jumbo = cpp >= 256;
-        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (jumbo ? 33u : 17u);
+        const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (jumbo ? 33u : 25u);
         const FlatVariant* fv = &flat_variant(loads);
         const uint32_t flags = g_tune.flags.load();
         const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 128u : 64u);
@@ -1150,9 +1151,11 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
                          hipStream_t s) {
     const uint64_t tiles = (n + 63) / 64;
     // loads_per_lane: 2/4/8/16 rows in flight on packed tiles (at most 4 on
-    // others), 3/5/7/9/13/17 = ring-pipelined 2/4/6/8/12/16.  Default: ring of
-    // 12 (cfg4 +2.5 % over plain 4, profiles/r01_ragged_ring_scan.jsonl)
-    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 13u;
+    // others), 3/5/7/9/13/17/25/33 = ring-pipelined 2/4/6/8/12/16/24/32.
+    // Default: ring of 24 (cfg4: ring 12 +2.5 % over plain 4,
+    // profiles/r01_ragged_ring_scan.jsonl; ring 24 +1.4 % over 12/16 and ring
+    // 32 -14 %, r01_deep_ring_scan.jsonl)
+    const uint32_t u = g_tune.loads.load() ? g_tune.loads.load() : 25u;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {
@@ -1165,6 +1168,8 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
         case 7: launch_ragged_u<6, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         case 13: launch_ragged_u<12, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         case 17: launch_ragged_u<16, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 25: launch_ragged_u<24, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 33: launch_ragged_u<32, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
         default: launch_ragged_u<4, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
     }
     PIPCK_LAUNCHED("k_ragged");

@@ -205,7 +205,7 @@ def test_fixed_every_shape_vs_oracle(oracle, lanes):
         engine.tune()
 
 
-@pytest.mark.parametrize("rows", [2, 4, 8, 16, 3, 5, 9, 13, 17, 33])
+@pytest.mark.parametrize("rows", [2, 4, 8, 16, 3, 5, 9, 13, 17, 25, 33, 41])
 @pytest.mark.parametrize("nt", [False, True])
 @pytest.mark.parametrize("xcd", [False, True])
 def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
@@ -391,7 +391,7 @@ def test_ragged_vs_oracle(oracle, n):
 
 @pytest.mark.parametrize("blocks", [1, 3, 8, 9, 17])
 @pytest.mark.parametrize("xcd", [True, False])
-@pytest.mark.parametrize("rows", [2, 4, 8, 3, 5, 9, 7, 13, 17])
+@pytest.mark.parametrize("rows", [2, 4, 8, 3, 5, 9, 7, 13, 17, 25, 33])
 @pytest.mark.parametrize("wide", [False, True])
 def test_ragged_launch_shapes(oracle, blocks, xcd, rows, wide):
     """Every ragged row depth (plain and pipelined), 1- and 4-wave blocks, grids
@@ -433,7 +433,7 @@ def _packed_case(rng, n, max_len=3000):
     return offs, lens, pos + 16
 
 
-@pytest.mark.parametrize("rows", [4, 8, 3, 5, 9, 7, 13, 17])
+@pytest.mark.parametrize("rows", [4, 8, 3, 5, 9, 7, 13, 17, 25, 33])
 def test_ragged_packed_tiles(oracle, rows):
     rng = np.random.default_rng(rows)
     n = 64 * 40 + 9
