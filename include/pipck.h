@@ -143,8 +143,8 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
 /* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
  * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
- * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9/13/17/25/33/41 =
- * ring-pipelined 2/4/8/12/16/24/32/40); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
+ * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9/13/17/25/33 =
+ * ring-pipelined 2/4/8/12/16/24/32); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
  * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
  * fixed kernel, bit 3 = XCD-grouped task split, bit 4 = no packed-tile
  * addressing in the ragged kernel, bit 5 = 4-wave ragged blocks (default 1),

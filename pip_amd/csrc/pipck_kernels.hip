@@ -978,10 +978,12 @@ struct FlatVariant {
             {k_flat<U, P, true, false>, k_flat<U, P, true, true>}                         \
         }                                                                                 \
     }
-// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/25/33/41 = ring-pipelined U = 2/4/8/12/16/24/32/40
+// loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/25/33 = ring-pipelined U = 2/4/8/12/16/24/32
+// (a ring of 40 or 48 -- 231 / 272 VGPRs -- ran cfg5 1 % / 28 % slower than 32,
+// profiles/r01_flat_one_wave_scan.jsonl, r01_deep_ring_scan.jsonl)
 static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_F(8, false), PIPCK_F(16, false),
                                     PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
-                                    PIPCK_F(16, true), PIPCK_F(32, true), PIPCK_F(24, true), PIPCK_F(40, true)};
+                                    PIPCK_F(16, true), PIPCK_F(32, true), PIPCK_F(24, true)};
 #undef PIPCK_F
 static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
     {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
@@ -1000,7 +1002,7 @@ static const FlatVariant& flat_variant(uint32_t loads) {
         case 17: return kFlat[8];
         case 33: return kFlat[9];
         case 25: return kFlat[10];
-        case 41: return kFlat[11];
+
         default: return kFlat[2];
     }
 }
