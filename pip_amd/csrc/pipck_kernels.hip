@@ -410,8 +410,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
         const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, flow_origin, lane);
         u32x4 v[U];
         flat_load_rows<U, NT>(v, tb, 0, tchunks, lp, cpp, nch, lane);
-        for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
-            if (PIPE) {  // ring: a reduced row's registers take the load U rows ahead at once
+        if (PIPE && U >= 32) {  // deep ring: one loop, the last batch's reloads are clamped dummies
+            for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t rs = r0 + u * 64;  // wave-uniform
@@ -419,7 +419,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
                     pp.advance(cpp);
                     flat_load_row<NT>(v[u], tb, rs + 64 * U, tchunks, lp, cpp, nch, lane);  // unconditional (clamped)
                 }
-            } else {
+            }
+        } else if (PIPE) {
+            // Ring: a reduced row's registers take the load U rows ahead at once.
+            // While rows remain beyond the current batch every reload is issued
+            // (clamped to the task's last chunk past its end, so the VM count
+            // stays static and each reduce waits for its own row only); the
+            // final batch is reduced without reloads -- cfg2 (ring 24) +0.6-2.1 %;
+            // for the ring of 32 the second unrolled copy cost 0.6-1.2 %
+            // (profiles/r01_ab_flat_tail_batch.jsonl), so it keeps one loop.
+            uint32_t r0 = 0;
+            for (; r0 + 64 * U < tchunks; r0 += 64 * U) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const uint32_t rs = r0 + u * 64;  // < tchunks here
+                    flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                    pp.advance(cpp);
+                    flat_load_row<NT>(v[u], tb, rs + 64 * U, tchunks, lp, cpp, nch, lane);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rs = r0 + u * 64;  // wave-uniform
+                if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                pp.advance(cpp);
+            }
+        } else {
+            for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
                 flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
                 if (r0 + 64 * U < tchunks) flat_load_rows<U, NT>(v, tb, r0 + 64 * U, tchunks, lp, cpp, nch, lane);
             }
