@@ -151,7 +151,10 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
  * bit 6 = never the small-packet kernel (packets <= 64 B incl. chunk offset),
  * bit 7 = never the short-stride flat kernel (16-B-multiple strides < 1 KiB),
  * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bit 16 = no
- * lane-per-segment path for ragged tiles of tiny segments, bits 24..27 =
+ * lane-per-segment path for ragged tiles of tiny segments, bit 17 = never the
+ * tiny-stride flat kernel (8-B-multiple strides <= 64 B with pseudo-headers or
+ * RX verify; loads_per_lane 4/8/16 = its ring, bits 8..15 its rows per wave
+ * task, default 4 and 12), bit 18 = that kernel without pseudo-headers too, bits 24..27 =
  * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 

@@ -13,6 +13,9 @@
 //   k_flat_small<U>   fixed 16-B-multiple strides 64 B .. 1 KiB: the same row
 //                     stream with many packets per row, reduced by packet with
 //                     a DPP prefix scan into LDS partials.
+//   k_flat_tiny<U>    8-B-multiple strides up to 64 B with pseudo-headers or
+//                     RX verify: the row stream copied into an LDS stage that
+//                     holds whole packets, then lane-per-packet sums from LDS.
 //   k_small<NL,K>     packets <= 64 B incl. their first chunk's offset (cfg1's
 //                     20-B headers): one lane per packet, every load of the
 //                     wave task in flight before the first reduce.
@@ -554,6 +557,150 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
 }
 
 // ---------------------------------------------------------------------------
+// flat-stream kernel for tiny fixed strides (8-byte multiples, 8 .. 128 B)
+// ---------------------------------------------------------------------------
+// cfg1's 20-byte IPv4 headers at a 24-byte stride.  A wave task of `run`
+// consecutive packets is streamed as coalesced 1 KiB rows through a ring of U
+// rows in flight, as in k_flat, and each arriving row is copied to an LDS
+// stage (one ds_write_b128).  The stage holds a group of G rows that is a
+// whole number P of packets (G x 1 KiB = P x stride, P = 64 or 128), so when
+// a group is complete lane j sums packet j straight out of LDS: ceil(len/8)
+// 8-byte reads from the packet's start, the last one masked to `len` -- the
+// same mask for every packet, no per-lane offsets.  Each dword is folded by
+// v_dot2_u32_u16 against (1,1): lo16 + hi16 (+ acc) in one instruction,
+// residue- and zero-preserving (pipck_device.hpp).  Folded sums wait in LDS;
+// pseudo-header lookups and the 2-byte stores run at the task's end (loads and
+// stores share VM_CNT on gfx9: a store between row loads would make the next
+// row's wait drain the ring).  The lane-per-packet kernels (k_small) spend
+// ~60 VALU per 1 KiB row on per-lane offsets and masks and stall on issue at
+// ~4.2 TB/s; this keeps the VALU work per row to the fold itself.
+constexpr uint32_t kNoFlatTiny = 1u << 17;     // pipck_tune flags bit 17: never k_flat_tiny
+constexpr uint32_t kForceFlatTiny = 1u << 18;  // bit 18: k_flat_tiny without pseudo-headers too
+constexpr uint32_t kFlatTinyMaxHalves = 8;  // strides up to 64 B
+constexpr uint32_t kFlatTinyMaxRun = 2048;  // packets per wave task
+
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot_fold(uint32_t w, uint32_t acc) {  // lo16(w) + hi16(w) + acc
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), u16x2{1, 1}, acc, false);
+}
+// Rows per LDS group for a stride of hpp 8-byte halves: the fewest whole rows
+// holding a whole number of packets, doubled until that is >= 64 packets.
+__host__ __device__ constexpr uint32_t tiny_group_rows(uint32_t hpp) {
+    uint32_t odd = hpp, pow2 = 1;
+    while (!(odd & 1u)) {
+        odd >>= 1;
+        pow2 <<= 1;
+    }
+    return odd * (pow2 > 1 ? pow2 / 2 : 1u);
+}
+// LDS per wave: the group stage plus one u16 per packet of the task
+__host__ __device__ constexpr uint32_t tiny_wave_lds(uint32_t hpp, uint32_t run) {
+    return tiny_group_rows(hpp) * 1024u + ((run * 2u + 15u) & ~15u);
+}
+
+template <int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) void k_flat_tiny(const uint8_t* __restrict__ arena, uint32_t hpp, uint32_t len,
+                                                   uint64_t n, uint32_t run, const uint32_t* __restrict__ pseudo,
+                                                   uint32_t n_flows, const uint32_t* __restrict__ flow_of,
+                                                   uint64_t flow_origin, uint16_t* __restrict__ out,
+                                                   uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint32_t s_tiny[];  // 4 waves x tiny_wave_lds(hpp, run) bytes (launch_fixed sizes it)
+    const int lane = threadIdx.x & 63;
+    const uint32_t stride = 8u * hpp;
+    const uint32_t G = tiny_group_rows(hpp), P = G * 128u / hpp;  // rows / packets per group
+    uint8_t* stage = reinterpret_cast<uint8_t*>(s_tiny) + (threadIdx.x >> 6) * tiny_wave_lds(hpp, run);
+    uint16_t* fs = reinterpret_cast<uint16_t*>(stage + G * 1024u);
+    const uint32_t nq = (len + 7) >> 3;  // 8-byte reads per packet (len >= 1)
+    const uint64_t mlast = low_bytes64((int)(len - 8 * (nq - 1)));
+    const uint32_t lterm = len_term(len);
+    const uint64_t n_tasks = (n + run - 1) / run;
+    const TaskRange tr = xcd_tasks(n_tasks, (kflags & kXcdGroups) != 0);
+    for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
+        const uint64_t p0 = task * run;
+        const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)run, n - p0);
+        const uint32_t tchunks = (np * stride + 15) >> 4;
+        // last chunk holding packet bytes: loads past it are clamped to it, so
+        // the batch's trailing padding is never touched
+        const uint32_t cmax = ((np - 1) * stride + len - 1) >> 4;
+        const u32x4* tb = reinterpret_cast<const u32x4*>(arena + p0 * stride);
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t c = min((uint32_t)(u * 64 + lane), cmax);
+            v[u] = NT ? load_stream(tb + c) : load_plain(tb + c);
+        }
+        uint32_t slot = 0, g0 = 0;  // row within the group; first packet of the group
+        for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t rs = r0 + u * 64;
+                if (rs < tchunks) {  // wave-uniform
+                    *reinterpret_cast<u32x4*>(stage + slot * 1024u + lane * 16) = v[u];
+                    if (++slot == G || rs + 64 >= tchunks) {  // group complete (or the task's last row)
+                        wave_sync();
+                        const uint32_t cnt = min(P, np - g0);
+                        for (uint32_t j = lane; j < cnt; j += 64) {
+                            const uint8_t* pk = stage + j * stride;
+                            uint32_t acc = 0;
+                            for (uint32_t q = 0; q + 1 < nq; q++) {
+                                const uint2 x = *reinterpret_cast<const uint2*>(pk + 8 * q);
+                                acc = dot_fold(x.x, dot_fold(x.y, acc));
+                            }
+                            const uint2 x = *reinterpret_cast<const uint2*>(pk + 8 * (nq - 1));
+                            acc = dot_fold(x.x & (uint32_t)mlast, dot_fold(x.y & (uint32_t)(mlast >> 32), acc));
+                            fs[g0 + j] = (uint16_t)bswap16(fold16(acc));  // packets start 8-byte aligned: even
+                        }
+                        wave_sync();
+                        slot = 0;
+                        g0 += P;
+                    }
+                }
+                const uint32_t c = min(rs + 64 * U + lane, cmax);  // ring: unconditional (clamped) reload
+                v[u] = NT ? load_stream(tb + c) : load_plain(tb + c);
+            }
+        }
+        // results: 4 consecutive packets per lane and one 8-byte (4-byte for
+        // RX verify) store where the output is aligned, the rest one by one
+        auto result = [&](uint32_t i, uint32_t flow) -> uint32_t {
+            const uint32_t F = fs[i];
+            uint32_t P_ = 0;
+            if (pseudo) P_ = pseudo[flow_of ? flow_of[p0 + i] : flow] + lterm;
+            return VERIFY ? (uint32_t)(fold16(P_ + F) == 0xFFFFu) : (uint32_t)finish(P_, F);
+        };
+        const bool vec = ((VERIFY ? (uintptr_t)ok : (uintptr_t)out) & (VERIFY ? 3u : 7u)) == 0;  // p0 % 64 == 0
+        const uint32_t nvec = vec ? np & ~3u : 0u;
+        uint32_t flow = 0;
+        const uint32_t fstep4 = pseudo && !flow_of ? 256u % n_flows : 0u;
+        if (pseudo && !flow_of) flow = (uint32_t)((flow_origin + p0 + 4u * lane) % n_flows);
+        for (uint32_t i = 4u * lane; i < nvec; i += 256) {
+            uint32_t r[4], f = flow;
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                r[t] = result(i + t, f);
+                if (++f == n_flows) f = 0;
+            }
+            if (VERIFY)
+                *reinterpret_cast<uint32_t*>(ok + p0 + i) = r[0] | r[1] << 8 | r[2] << 16 | r[3] << 24;
+            else
+                *reinterpret_cast<uint2*>(out + p0 + i) = make_uint2(r[0] | r[1] << 16, r[2] | r[3] << 16);
+            flow += fstep4;
+            if (flow >= n_flows) flow -= n_flows;
+        }
+        if (pseudo && !flow_of) flow = (uint32_t)((flow_origin + p0 + nvec + lane) % n_flows);
+        for (uint32_t i = nvec + lane; i < np; i += 64) {
+            const uint32_t x = result(i, flow);
+            if (VERIFY)
+                ok[p0 + i] = (uint8_t)x;
+            else
+                out[p0 + i] = (uint16_t)x;
+            flow += pseudo && !flow_of ? 64u % n_flows : 0u;
+            if (flow >= n_flows) flow -= n_flows;
+        }
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ragged / chain-segment kernel
 // ---------------------------------------------------------------------------
 struct RaggedTileLds {
@@ -1014,6 +1161,10 @@ static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_
 static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
     {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
     {k_flat_small<16, true, false>, k_flat_small<16, true, true>}};
+#define PIPCK_T(R) \
+    { {k_flat_tiny<R, false, false>, k_flat_tiny<R, false, true>}, {k_flat_tiny<R, true, false>, k_flat_tiny<R, true, true>} }
+static const flat_fn kFlatTiny[3][2][2] = {PIPCK_T(4), PIPCK_T(8), PIPCK_T(16)};  // [ring 4/8/16][verify][nt]
+#undef PIPCK_T
 
 static const FlatVariant& flat_variant(uint32_t loads) {
     switch (loads) {
@@ -1117,6 +1268,31 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
                            as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
                            n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat_small");
+        return PIPCK_OK;
+    }
+    // Tiny 8-B-multiple strides with pseudo-headers (pure ACKs, small UDP) or
+    // RX verify: the LDS-staged row stream.  cfg1 on 24-B strides, 256M
+    // packets: with IPv4 pseudo-headers 1.29 vs 1.40 ms for k_small (+8.5 %),
+    // verify 1.13 vs 1.15 ms; the bare IPv4-header checksum (no pseudo-header)
+    // ran 1.24-1.34 vs 1.22 ms, so it stays on k_small
+    // (profiles/r01_flat_tiny_scan.jsonl).
+    if ((uintptr_t)d_arena % 16 == 0 && stride % 8 == 0 && stride >= 8 && stride <= 8 * kFlatTinyMaxHalves &&
+        len >= 1 && len <= stride && (d_pseudo || verify || (g_tune.flags.load() & kForceFlatTiny)) &&
+        !g_tune.lanes.load() && !(g_tune.flags.load() & kNoFlatTiny)) {
+        const uint32_t hpp = (uint32_t)(stride / 8);
+        const uint32_t flags = g_tune.flags.load();
+        const uint32_t lq = g_tune.loads.load();
+        const int ui = lq == 8 ? 1 : (lq == 16 ? 2 : 0);  // ring of 4 rows by default
+        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 12u;
+        // whole LDS groups per task (so tasks start 1 KiB aligned), ~`rows` rows
+        const uint32_t G = tiny_group_rows(hpp), P = G * 128u / hpp;
+        const uint32_t run = std::max(1u, std::min(kFlatTinyMaxRun / P, rows / G)) * P;
+        const uint64_t tasks = (n + run - 1) / run;
+        const size_t lds = 4u * tiny_wave_lds(hpp, run);
+        hipLaunchKernelGGL(kFlatTiny[ui][verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), lds,
+                           as_stream(stream), (const uint8_t*)d_arena, hpp, len, n, run, d_pseudo,
+                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+        PIPCK_LAUNCHED("k_flat_tiny");
         return PIPCK_OK;
     }
     // Largest in-chunk offset any packet start can have: starts are

@@ -188,10 +188,11 @@ def gen_ragged(n: int, first: int, seed: int, hdr: int, n_flows: int, device=Non
 def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, plain_loads: bool = False,
          flat: bool = True, nt_loads: bool = False, rows_per_task: int = 0, xcd_groups: bool = False,
          packed_tiles: bool = True, wide_blocks: bool = False,
-         small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True) -> None:
+         small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True,
+         flat_tiny: bool = True, force_flat_tiny: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic); see pipck_tune in include/pipck.h."""
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
              | (0 if packed_tiles else 16) | (32 if wide_blocks else 0) | (0 if small else 64)
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
-             | (small_k_log << 24))
+             | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)

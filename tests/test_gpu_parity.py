@@ -237,12 +237,74 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
         engine.tune()
 
 
+@pytest.mark.parametrize("ring,rows,nt", [(0, 0, True), (4, 4, True), (16, 64, True), (8, 2, False), (16, 8, True)])
+def test_tiny_stride_flat_kernel_vs_oracle(oracle, ring, rows, nt):
+    """k_flat_tiny (8-byte-multiple strides 8..64 B, 16-byte-aligned arena;
+    forced on for batches without pseudo-headers too; rings of 4/8/16 rows,
+    tasks of 2..64 rows in whole LDS groups; strides up to 128 B reach the
+    other fixed kernels): every stride, lengths 1 / 20 / stride-1 / stride and
+    random ones, batch sizes around the task size, one task per wave and a
+    capped grid that loops, implicit and explicit flows, RX verify, results
+    aligned (vector stores) and shifted by one element (scalar stores)."""
+    rng = np.random.default_rng(900 + rows + ring)
+    try:
+        for stride in range(8, 129, 8):
+            hpp = stride // 8
+            odd, pow2 = hpp, 1
+            while odd % 2 == 0:
+                odd, pow2 = odd // 2, pow2 * 2
+            G = odd * max(1, pow2 // 2)  # rows per LDS group (tiny_group_rows)
+            P = G * 128 // hpp
+            run = max(1, min(2048 // P, (rows or 12) // G)) * P  # mirrors launch_fixed
+            lengths = sorted({1, min(20, stride), stride - 1 or 1, stride, int(rng.integers(1, stride + 1))})
+            for length in lengths:
+                n = int(rng.choice([1, 2, run - 1, run, run + 1, 3 * run + 5, 20000]))
+                blocks = int(rng.choice([0, 0, 1, 7]))
+                engine.tune(0, ring, blocks, plain_loads=not nt, nt_loads=nt, rows_per_task=rows,
+                            force_flat_tiny=True)
+                fam = int(rng.choice([0, 4, 6]))
+                host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+                if n > 3:
+                    host[stride:2 * stride] = 0xFF
+                    host[2 * stride:3 * stride] = 0
+                _, arena = upload(host, 0)
+                seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
+                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+                # results 8-/4-byte aligned (vector stores) or shifted by one element (scalar stores)
+                shift = int(rng.integers(0, 2))
+                out = torch.empty(n + 1, dtype=torch.int16, device=DEV)[shift:shift + n]
+                okb = torch.empty(n + 1, dtype=torch.uint8, device=DEV)[shift:shift + n]
+                got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin, out=out))
+                assert np.array_equal(got, want), (stride, length, n, blocks, shift, np.nonzero(got != want)[0][:5])
+                ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin, ok=okb)
+                assert np.array_equal(ok.cpu().numpy().astype(bool), got == 0)
+        # explicit per-packet flow indices on the cfg1 shape
+        n, L = 5003, 20
+        host = rng.integers(0, 256, n * 24, dtype=np.uint8)
+        _, arena = upload(host, 0)
+        _, pseudo = engine.gen_flows(6, N_FLOWS, 77, 17)
+        flow_of = rng.integers(0, N_FLOWS, n).astype(np.int32)
+        engine.tune(0, ring, 0, plain_loads=not nt, nt_loads=nt, rows_per_task=rows, force_flat_tiny=True)
+        got = u16(engine.checksum_fixed(arena, 24, L, n, pseudo, N_FLOWS, torch.from_numpy(flow_of).to(DEV), 0))
+        engine.tune(flat_tiny=False)
+        ref = u16(engine.checksum_fixed(arena, 24, L, n, pseudo, N_FLOWS, torch.from_numpy(flow_of).to(DEV), 0))
+        assert np.array_equal(got, ref)
+        for i in range(0, n, 11):
+            s, d = oracle.flow6(77, int(flow_of[i]))
+            assert got[i] == oracle.inet6_checksum(host[i * 24:i * 24 + L].tobytes(), 17, s, d)
+    finally:
+        engine.tune()
+
+
 @pytest.mark.parametrize("misalign", [0, 1, 4, 8, 13])
 def test_small_packet_kernel_vs_oracle(oracle, misalign):
     """k_small (one lane per packet, <= 64 bytes incl. the first chunk's offset):
     every length 0..49 at tight, odd, 8- and 16-aligned strides (and strides
     below 16), partial last tasks, implicit and explicit flows, RX verify; the
-    same batches through k_fixed (small=False) must agree."""
+    same batches through k_fixed (small=False) must agree.  With a 16-byte
+    aligned arena the 8-byte-multiple strides take k_flat_tiny by default, so
+    k_small runs there with flat_tiny=False."""
     rng = np.random.default_rng(500 + misalign)
     try:
         for length in range(0, 50):
@@ -263,9 +325,10 @@ def test_small_packet_kernel_vs_oracle(oracle, misalign):
                 assert np.array_equal(got, want), (length, stride, n, fam, np.nonzero(got != want)[0][:5])
                 ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
                 assert np.array_equal(ok.astype(bool), got == 0)
-                engine.tune(small=False)
-                old = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
-                assert np.array_equal(old, want)
+                for arm in (dict(flat_tiny=False), dict(flat_tiny=False, small=False)):
+                    engine.tune(**arm)
+                    old = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                    assert np.array_equal(old, want), (arm, length, stride, n)
         # explicit per-packet flow indices
         n, L = 3001, 20
         host = rng.integers(0, 256, n * 24, dtype=np.uint8)

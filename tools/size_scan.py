@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma list of cfgN (default cfg5,cfg4)")
     ap.add_argument("--sizes", default="", help="comma list of packet counts in Mi (default per workload)")
+    ap.add_argument("--pseudo", action="store_true", help="fixed-stride workloads: add IPv4 pseudo-headers even for cfg1")
     ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs}, or @file (default: built-in arms)")
     a = ap.parse_args()
     engine.require_gpu()
@@ -54,7 +55,8 @@ def main():
     if a.sizes:
         plan = [(w, tuple(int(float(x) * (1 << 20)) for x in a.sizes.split(","))) for w, _ in plan]
     for w, sizes in plan:
-        pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
+        fam = w.family or (4 if a.pseudo else 0)  # cfg1: IP header, no pseudo-header
+        pseudo = engine.gen_flows(fam, N_FLOWS, w.seed, w.proto or 6)[1] if fam else None
         for n in sizes:
             if w.ragged:
                 arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
