@@ -196,9 +196,9 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena
         const uint64_t pkt = base + 64u * k + lane;
         if (pkt < n) {
             if (VERIFY)
-                ok[pkt] = (uint8_t)res[k];
+                __builtin_nontemporal_store((uint8_t)res[k], &ok[pkt]);
             else
-                out[pkt] = (uint16_t)res[k];
+                __builtin_nontemporal_store((uint16_t)res[k], &out[pkt]);
         }
     }
 }
@@ -680,9 +680,11 @@ __global__ __launch_bounds__(256) void k_flat_tiny(const uint8_t* __restrict__ a
                 if (++f == n_flows) f = 0;
             }
             if (VERIFY)
-                *reinterpret_cast<uint32_t*>(ok + p0 + i) = r[0] | r[1] << 8 | r[2] << 16 | r[3] << 24;
+                __builtin_nontemporal_store(r[0] | r[1] << 8 | r[2] << 16 | r[3] << 24,
+                                            reinterpret_cast<uint32_t*>(ok + p0 + i));
             else
-                *reinterpret_cast<uint2*>(out + p0 + i) = make_uint2(r[0] | r[1] << 16, r[2] | r[3] << 16);
+                __builtin_nontemporal_store((uint64_t)(r[2] | r[3] << 16) << 32 | (r[0] | r[1] << 16),
+                                            reinterpret_cast<uint64_t*>(out + p0 + i));
             flow += fstep4;
             if (flow >= n_flows) flow -= n_flows;
         }
@@ -690,9 +692,9 @@ __global__ __launch_bounds__(256) void k_flat_tiny(const uint8_t* __restrict__ a
         for (uint32_t i = nvec + lane; i < np; i += 64) {
             const uint32_t x = result(i, flow);
             if (VERIFY)
-                ok[p0 + i] = (uint8_t)x;
+                __builtin_nontemporal_store((uint8_t)x, &ok[p0 + i]);
             else
-                out[p0 + i] = (uint16_t)x;
+                __builtin_nontemporal_store((uint16_t)x, &out[p0 + i]);
             flow += pseudo && !flow_of ? 64u % n_flows : 0u;
             if (flow >= n_flows) flow -= n_flows;
         }

@@ -24,7 +24,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-WORKLOADS = {"cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20}
+WORKLOADS = {"cfg1": 256 << 20, "cfg1p": 256 << 20, "cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20}
 
 
 def worker(only: list[str], iters: int) -> None:
@@ -38,8 +38,9 @@ def worker(only: list[str], iters: int) -> None:
 
     engine.require_gpu()
     for name in only:
-        w, n = BY_CFG[int(name[3:])], WORKLOADS[name]
-        pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1]
+        w, n = BY_CFG[int(name[3:4])], WORKLOADS[name]
+        fam = w.family or (4 if name.endswith("p") else 0)  # cfg1p: cfg1 with IPv4 pseudo-headers
+        pseudo = engine.gen_flows(fam, N_FLOWS, w.seed, w.proto or 6)[1] if fam else None
         if w.ragged:
             arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
@@ -51,7 +52,8 @@ def worker(only: list[str], iters: int) -> None:
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
         ms = statistics.median(timed(run, iters) for _ in range(3))
         digest = hashlib.sha256(run().cpu().numpy().tobytes()).hexdigest()[:16]
-        print(json.dumps({"workload": w.name, "packets": n, "ms": ms, "bytes": nbytes, "sha": digest}), flush=True)
+        print(json.dumps({"workload": w.name + ("+pseudo" if fam and not w.family else ""), "packets": n, "ms": ms,
+                          "bytes": nbytes, "sha": digest}), flush=True)
         del arena
         torch.cuda.empty_cache()
 
