@@ -247,6 +247,13 @@ int pipck_txq_add4_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8
                       uint32_t dst, void* csum_field);
 int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
                       const uint8_t* dst, void* csum_field);
+/* Automatic zero-copy (off by default; on at creation when the environment sets
+ * PIPCK_TXQ_AUTO_ZERO_COPY=1): pipck_txq_add4/add6 then read every segment that
+ * lies in a pinned range in place and copy the others, so pinned segments follow
+ * the zero-copy contract above (valid and unchanged until their batch
+ * completes).  Lets callers that cannot choose the _zc forms -- pip's deferred
+ * drop-in -- use pinned utun/socket buffers without a copy. */
+int pipck_txq_auto_zero_copy(pipck_txq* q, int on);
 /* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);
 /* packets added since the last submit/flush */

@@ -84,6 +84,7 @@ SIGNATURES = {
     "pipck_txq_submit": (_i32, [_p]),
     "pipck_txq_complete": (_i32, [_p]),
     "pipck_txq_inflight": (_u64, [_p]),
+    "pipck_txq_auto_zero_copy": (_i32, [_p, _i32]),
 }
 
 _lib = None

@@ -46,6 +46,9 @@ void pinned_add(const void* p, size_t bytes);
 void pinned_remove(const void* p);
 // true if [p, p+len) lies inside one registered range; *hit returns that range
 bool pinned_lookup(const void* p, size_t len, PinnedRange* hit);
+// Changes whenever a range is removed: callers caching ranges drop their cache
+// then, so a freed (and perhaps reused, unpinned) buffer is never read in place.
+uint64_t pinned_generation();
 
 // pipck_checksum_chains without argument checks, for callers whose segment
 // descriptors hold absolute device-accessible addresses (d_arena == nullptr):

@@ -36,6 +36,9 @@ void set_error(const std::string& msg) { t_err = msg; }
 
 static std::shared_mutex g_pinned_mu;
 static std::map<uintptr_t, uintptr_t> g_pinned;  // lo -> hi
+static std::atomic<uint64_t> g_pinned_gen{0};     // bumped by every removal
+
+uint64_t pinned_generation() { return g_pinned_gen.load(std::memory_order_acquire); }
 
 void pinned_add(const void* p, size_t bytes) {
     std::unique_lock<std::shared_mutex> g(g_pinned_mu);
@@ -45,6 +48,7 @@ void pinned_add(const void* p, size_t bytes) {
 void pinned_remove(const void* p) {
     std::unique_lock<std::shared_mutex> g(g_pinned_mu);
     g_pinned.erase((uintptr_t)p);
+    g_pinned_gen.fetch_add(1, std::memory_order_acq_rel);
 }
 
 bool pinned_lookup(const void* p, size_t len, PinnedRange* hit) {

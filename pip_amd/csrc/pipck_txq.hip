@@ -134,6 +134,8 @@ struct pipck_txq {
     TxBatch batch[2];
     PinnedRange pin_cache[4];  // pinned ranges of recent zero-copy segments (headers and payloads
     unsigned pin_next = 0;     // usually come from a few buffers): most checks skip the registry
+    uint64_t pin_gen = 0;      // registry generation the cache was filled under
+    bool auto_zc = false;      // plain adds read pinned segments in place (pipck_txq_auto_zero_copy)
     int cur = 0;         // batch receiving adds
     bool inflight = false;  // batch[cur ^ 1] has been submitted and not completed
 };
@@ -151,34 +153,50 @@ int append_bytes(TxBatch* b, const void* src, uint32_t len, uint64_t* off) {
     return PIPCK_OK;
 }
 
+// Is [p, p+len) inside a pinned range (pipck_host_alloc / pipck_host_register)?
+// The queue's 4-entry cache answers most checks; it is dropped whenever a range
+// has been removed since it was filled.
+bool seg_pinned(pipck_txq* q, const void* p, uint32_t len) {
+    const uint64_t gen = pinned_generation();
+    if (gen != q->pin_gen) {
+        for (PinnedRange& r : q->pin_cache) r = PinnedRange{};
+        q->pin_gen = gen;
+    }
+    const uintptr_t a = (uintptr_t)p;
+    for (const PinnedRange& r : q->pin_cache)
+        if (a >= r.lo && a + len <= r.hi) return true;
+    PinnedRange r;
+    if (!pinned_lookup(p, len, &r)) return false;
+    q->pin_cache[q->pin_next++ % 4] = r;
+    return true;
+}
+
+// zc: every segment is read in place (refused unless pinned); otherwise, in a
+// queue with auto_zc set, pinned segments are read in place and others copied.
 int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo& ps, void* field, bool zc) {
     if (!q || !field || (nseg && !segs)) {
         set_error("pipck_txq_add: null argument");
         return PIPCK_EINVAL;
     }
+    uint32_t in_place = 0;  // bit i: segment i is read in place (nseg <= 32 when any is)
     for (uint32_t i = 0; i < nseg; i++) {
         if (segs[i].len > PIPCK_MAX_SEG_LEN || (segs[i].len && !segs[i].ptr)) {
             set_error("pipck_txq_add: segment null or longer than 65535 bytes");
             return PIPCK_ERANGE;
         }
-        if (zc && segs[i].len) {  // the GPU will read it in place: it must be pinned
-            const uintptr_t a = (uintptr_t)segs[i].ptr;
-            bool ok = false;
-            for (const PinnedRange& r : q->pin_cache) ok |= a >= r.lo && a + segs[i].len <= r.hi;
-            if (!ok) {
-                PinnedRange r;
-                if (!pinned_lookup(segs[i].ptr, segs[i].len, &r)) {
-                    set_error("pipck_txq_add_zc: segment outside every range from pipck_host_alloc / "
-                              "pipck_host_register");
-                    return PIPCK_EINVAL;
-                }
-                q->pin_cache[q->pin_next++ % 4] = r;
-            }
+        if (zc && segs[i].len && !seg_pinned(q, segs[i].ptr, segs[i].len)) {
+            // the GPU will read it in place: it must be pinned
+            set_error("pipck_txq_add_zc: segment outside every range from pipck_host_alloc / "
+                      "pipck_host_register");
+            return PIPCK_EINVAL;
         }
+        if (!zc && q->auto_zc && i < 32 && segs[i].len && seg_pinned(q, segs[i].ptr, segs[i].len))
+            in_place |= 1u << i;
     }
     TxBatch* b = &q->batch[q->cur];
     for (uint32_t i = 0; i < nseg; i++) {
-        if (zc) {  // read in place at flush time (pinned host memory, device-accessible at the same address)
+        if (zc || (i < 32 && (in_place >> i & 1u))) {
+            // read in place at flush time (pinned host memory, device-accessible at the same address)
             b->inet_segs.push_back(pipck_desc{(uint64_t)(uintptr_t)segs[i].ptr, segs[i].len, 1u});
             b->has_zc = true;
             continue;
@@ -316,6 +334,8 @@ int pipck_txq_create(pipck_ctx* ctx, pipck_txq** out) {
     pipck_txq* q = new pipck_txq();
     q->ctx = ctx;
     q->device = dev;
+    q->pin_gen = pinned_generation();
+    if (const char* e = getenv("PIPCK_TXQ_AUTO_ZERO_COPY")) q->auto_zc = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&q->done, hipEventDisableTiming) != hipSuccess) {
         set_error("pipck_txq_create: stream/event creation failed");
@@ -324,6 +344,15 @@ int pipck_txq_create(pipck_ctx* ctx, pipck_txq** out) {
         return PIPCK_EHIP;
     }
     *out = q;
+    return PIPCK_OK;
+}
+
+int pipck_txq_auto_zero_copy(pipck_txq* q, int on) {
+    if (!q) {
+        set_error("pipck_txq_auto_zero_copy: null queue");
+        return PIPCK_EINVAL;
+    }
+    q->auto_zc = on != 0;
     return PIPCK_OK;
 }
 

@@ -928,3 +928,86 @@ def test_txq_zero_copy_segments(oracle, register, in_place, monkeypatch):
             lib.pipck_host_unregister(C.c_void_p(base))
         else:
             lib.pipck_host_free(C.c_void_p(base))
+
+
+@pytest.mark.parametrize("env", [False, True])
+def test_txq_auto_zero_copy(oracle, env, monkeypatch):
+    """pipck_txq_auto_zero_copy (or PIPCK_TXQ_AUTO_ZERO_COPY=1 at creation):
+    plain add4/add6 read pinned segments in place and copy the rest.  Shown by
+    rewriting every source buffer after add and before flush: a pinned
+    segment's checksum follows the new bytes, a copied one keeps the add-time
+    bytes.  Then the pinned range is freed: the queue's range cache must drop
+    it, so a zero-copy add of the same address is refused (never read in place)."""
+    if env:
+        monkeypatch.setenv("PIPCK_TXQ_AUTO_ZERO_COPY", "1")
+    lib = _lib.load()
+    ctx, q = C.c_void_p(), C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    if not env:
+        _lib.check("auto_zero_copy", lib.pipck_txq_auto_zero_copy(q, 1))
+    size = 1 << 20
+    base = lib.pipck_host_alloc(size)
+    assert base
+    pool = np.ctypeslib.as_array((C.c_uint8 * size).from_address(base))
+    rng = np.random.default_rng(77 + env)
+    freed = False
+    try:
+        n_pk = 300
+        fields = (C.c_uint8 * (2 * n_pk))()
+        keep, finals, pos = [], [], 0
+        for i in range(n_pk):
+            field = C.c_void_p(C.addressof(fields) + 2 * i)
+            nseg = int(rng.integers(1, 4))
+            arr = (_lib.HSeg * nseg)()
+            segs_final = []
+            for j in range(nseg):
+                ln = int(rng.choice([0, 20, int(rng.integers(1, 1500))]))
+                old = rng.integers(0, 256, ln, dtype=np.uint8)
+                new = rng.integers(0, 256, ln, dtype=np.uint8)
+                if rng.integers(0, 2):  # pinned: read at flush -> the rewritten bytes count
+                    pos += int(rng.integers(0, 16))
+                    pool[pos:pos + ln] = old
+                    arr[j].ptr = C.c_void_p(base + pos)
+                    keep.append(("pinned", pos, new))
+                    pos += ln
+                    segs_final.append(new.tobytes())
+                else:  # ordinary memory: copied at add -> the add-time bytes count
+                    b = C.create_string_buffer(old.tobytes(), max(ln, 1))
+                    arr[j].ptr = C.cast(b, C.c_void_p)
+                    keep.append(("plain", b, new))
+                    segs_final.append(old.tobytes())
+                arr[j].len = ln
+            proto = int(rng.choice([6, 17]))
+            if i % 2:
+                s_, d_ = rng.bytes(4), rng.bytes(4)
+                _lib.check("add4", lib.pipck_txq_add4(q, arr, nseg, proto, int.from_bytes(s_, "little"),
+                                                      int.from_bytes(d_, "little"), field))
+                finals.append(oracle.inet_checksum_chain(segs_final, proto, s_, d_))
+            else:
+                s_, d_ = rng.bytes(16), rng.bytes(16)
+                _lib.check("add6", lib.pipck_txq_add6(q, arr, nseg, proto, s_, d_, field))
+                finals.append(oracle.inet6_checksum_chain(segs_final, proto, s_, d_))
+        for kind, where, new in keep:  # rewrite every source after add
+            if kind == "pinned":
+                pool[where:where + len(new)] = new
+            elif len(new):
+                C.memmove(where, new.tobytes(), len(new))
+        _lib.check("flush", lib.pipck_txq_flush(q))
+        got = np.frombuffer(bytes(fields), dtype=">u2")
+        assert np.array_equal(got, np.array(finals, dtype=np.uint16)), np.nonzero(got != finals)[0][:5]
+        # a freed range leaves the cache: zero-copy adds of it are refused
+        seg = (_lib.HSeg * 1)()
+        seg[0].ptr, seg[0].len = C.c_void_p(base + 64), 32
+        fld = (C.c_uint8 * 2)()
+        _lib.check("add4_zc", lib.pipck_txq_add4_zc(q, seg, 1, 6, 1, 2, C.cast(fld, C.c_void_p)))
+        _lib.check("flush", lib.pipck_txq_flush(q))
+        lib.pipck_host_free(C.c_void_p(base))
+        freed = True
+        assert lib.pipck_txq_add4_zc(q, seg, 1, 6, 1, 2, C.cast(fld, C.c_void_p)) == _lib.PIPCK_EINVAL
+        assert lib.pipck_txq_pending(q) == 0
+    finally:
+        lib.pipck_txq_destroy(q)
+        lib.pipck_ctx_destroy(ctx)
+        if not freed:
+            lib.pipck_host_free(C.c_void_p(base))

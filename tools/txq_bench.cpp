@@ -13,7 +13,10 @@
 //              while the previous one is in flight; pipck_txq_complete at the end;
 //   zero_copy  pipelined, with headers and payloads in pinned host memory
 //              (pipck_host_alloc) added by pipck_txq_add4_zc: the GPU reads
-//              them in place, nothing is copied at add time.
+//              them in place, nothing is copied at add time;
+//   auto_zc    pipelined, plain pipck_txq_add4 on queues in automatic
+//              zero-copy mode (pipck_txq_auto_zero_copy): the same in-place
+//              reads, decided per segment by the pinned-range lookup.
 // Every header's th_sum is checked against the first sync round.  Prints one
 // JSON line per mode: host-to-host rate of the whole add+flush cycle.
 #include <algorithm>
@@ -86,9 +89,10 @@ int main(int argc, char** argv) {
         }
     }
     std::vector<uint8_t> want;  // th_sum of every packet from the first sync round
-    static const char* kModes[] = {"sync", "pipelined", "zero_copy"};
-    for (int mode = 0; mode < 3; mode++) {
+    static const char* kModes[] = {"sync", "pipelined", "zero_copy", "auto_zc"};
+    for (int mode = 0; mode < 4; mode++) {
         const bool pipelined = mode >= 1, zc = mode == 2;
+        for (auto& s : shards) pipck_txq_auto_zero_copy(s.q, mode == 3);
         double best = 1e30;
         for (int r = 0; r < rounds; r++) {
             for (uint32_t i = 0; i < n; i++) hdr[(size_t)i * 20 + 16] = hdr[(size_t)i * 20 + 17] = 0;
