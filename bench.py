@@ -30,6 +30,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 from pip_amd import shard  # noqa: E402
+from pip_amd._lib import HDR_TCP, HDR_UDP  # noqa: E402
 from pip_amd.workloads import ALL, BY_CFG, N_FLOWS  # noqa: E402
 
 METRIC = "GiB/s payload checksummed (device-resident), MTU-9000 TCP batch; Mpkt/s"
@@ -115,6 +116,10 @@ def main() -> int:
     total_pkts = shard.sum_over_ranks(env, float(count))
 
     gib_s = total_bytes * args.steps / elapsed / 2**30
+    # L4 payload only: the checksummed bytes minus the TCP (20 B) /
+    # UDP (8 B) header of every packet; an IPv4-header batch (cfg1) has none
+    hdr_len = {HDR_TCP: 20, HDR_UDP: 8}.get(w.hdr, 0)
+    payload_gib_s = (total_bytes - hdr_len * total_pkts) * args.steps / elapsed / 2**30
     mpkt_s = total_pkts * args.steps / elapsed / 1e6
     algo_bytes = l4_bytes + 2 * count  # per launch on this rank
     achieved = algo_bytes / launch_s / 1e9
@@ -149,6 +154,7 @@ def main() -> int:
         },
         "mpkt_per_s": round(mpkt_s, 2),
         "per_gpu_gib_per_s": round(gib_s / env.world, 2),
+        "l4_payload_gib_per_s": round(payload_gib_s, 2),
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
