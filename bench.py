@@ -4,18 +4,28 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg5]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+With ``--gpus N > 1`` and no WORLD_SIZE in the environment, bench.py starts
+the N ranks itself (one child process per GPU, ``shard.spawn_ranks``; the
+parent never touches the GPU).  Under torch.distributed.run, WORLD_SIZE must
+equal --gpus.
+
 A step = one launch of the checksum kernel over this rank's whole shard of
 synthetic packets already resident in HBM (generated on the device from
 global packet ids; cfg5 = 8,980-byte TCP/IPv4 segments, 8M packets per GPU,
-64M at 8 GPUs -> weak scaling).  Ranks share nothing on the data path; gloo
-carries the barrier and the MAX of elapsed times.  Rank 0 prints ONE JSON line.
+64M at 8 GPUs -> weak scaling).  Ranks share nothing on the data path: fixed
+configs split the global packet-id range evenly, ragged ones (cfg4) at equal
+L4 bytes.  gloo carries the barrier, the MAX of elapsed times and the per-rank
+figures.  Rank 0 prints ONE JSON line.
 
 value   = checksummed L4 bytes of all ranks x K / max-over-ranks wall time, GiB/s
 roofline: algorithmic bytes per launch (L + 2 per packet: L read, u16 written)
-          / mean launch duration from HIP events on the launch stream, vs 8 TB/s
-cpu_baseline: pip's own pip_inet_checksum (oracle/_ref, compiled from the
-          reference) -- or the oracle's C restatement if _ref is absent -- on
-          a bounded sample of the same packets, all host cores; rank 0, N=1.
+          / the MEDIAN per-dispatch duration (a HIP event pair around every
+          launch, on the launch stream), vs 8 TB/s; the back-to-back mean is
+          reported beside it
+cpu_baseline: pip's own pip_inet_checksum / pip_ip_checksum (oracle/_ref,
+          compiled from the reference) -- or the oracle's C restatement if
+          _ref is absent -- on a bounded sample of the same packets, all host
+          cores and one core; rank 0, N=1.
 """
 from __future__ import annotations
 
@@ -38,18 +48,18 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PER_GPU_PACKETS = 8 << 20  # cfg5: 64M packets over 8 GPUs
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", default="cfg5", help="cfg2|cfg3|cfg4|cfg5 (default: the headline cfg5)")
+    p.add_argument("--workload", default="cfg5", help="cfg1..cfg5 (default: the headline cfg5)")
     p.add_argument("--packets-per-gpu", type=int, default=0, help="override the per-GPU shard size")
     p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and host end-to-end legs")
     p.add_argument("--traffic", default="auto",
                    help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def host_threads() -> int:
@@ -61,8 +71,26 @@ def host_threads() -> int:
     return max(1, min(n, cap) if cap else n)
 
 
-def main() -> int:
-    args = parse()
+def workload(name: str):
+    return ALL[name] if name in ALL else BY_CFG[int(name.lstrip("cfg"))]
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}", file=sys.stderr)
+            return 2
+    elif args.gpus > 1:
+        # one process per GPU; this parent process never initialises HIP
+        return shard.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]])
+    return run_rank(args)
+
+
+def run_rank(args) -> int:
     env = shard.dist_env()
     shard.init_control_plane(env)
 
@@ -71,22 +99,37 @@ def main() -> int:
     from pip_amd import engine
 
     # one GPU per rank; ranks beyond the visible devices share them (rehearsing N>1 on a 1-GPU box)
-    torch.cuda.set_device(env.local_rank % max(1, torch.cuda.device_count()))
+    n_dev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(env.local_rank % n_dev)
     engine.require_gpu()
-    w = ALL[args.workload] if args.workload in ALL else BY_CFG[int(args.workload.lstrip("cfg"))]
+    w = workload(args.workload)
     per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
     n_total = per_gpu * env.world
-    first, count = shard.shard_range(n_total, env.world, env.rank)
 
     # ---- this rank's shard, generated in HBM from global packet ids
     pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)[1] if w.family else None
     if w.ragged:
-        arena, desc, lens = engine.gen_ragged(count, first, w.seed, w.hdr, N_FLOWS)
+        # ragged: contiguous ranges of equal L4 bytes, cut on the
+        # prefix of every packet's length -- the same on every rank
+        if env.world > 1:
+            lens_all = torch.empty(n_total, dtype=torch.int32, device="cuda")
+            engine.call("pipck_gen_zipf_lengths", engine._ptr(lens_all), n_total, 0, w.seed,
+                        engine.current_stream())
+            prefix = torch.zeros(n_total + 1, dtype=torch.int64, device="cuda")
+            torch.cumsum(lens_all.to(torch.int64), 0, out=prefix[1:])
+            cuts = shard.byte_cuts(prefix, env.world)
+            first, count = cuts[env.rank], cuts[env.rank + 1] - cuts[env.rank]
+            lens = lens_all[first:first + count].clone()
+            del lens_all, prefix
+        else:
+            first, count, lens = 0, n_total, None
+        arena, desc, lens = engine.gen_ragged(count, first, w.seed, w.hdr, N_FLOWS, lengths=lens)
         l4_bytes = int(lens.to(torch.int64).sum().item())
 
         def step(out):
             return engine.checksum_ragged(arena, desc, pseudo, out=out)
     else:
+        first, count = shard.shard_range(n_total, env.world, env.rank)
         arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
         engine.gen_fixed(arena, w.stride, w.length, count, first, w.seed, w.hdr)
         l4_bytes = count * w.length
@@ -101,19 +144,26 @@ def main() -> int:
     torch.cuda.synchronize()
     shard.barrier(env)
 
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # an event pair around every launch, on the launch stream (engine launches on
+    # torch's current stream): per-dispatch durations without a profiler
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        ev_s[i].record()
         step(out)
-    ev1.record()
+        ev_e[i].record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     shard.barrier(env)
     elapsed = shard.max_over_ranks(env, t1 - t0)
-    launch_s = ev0.elapsed_time(ev1) / 1e3 / max(args.steps, 1)  # mean launch duration on the launch stream
-    total_bytes = shard.sum_over_ranks(env, float(l4_bytes))
-    total_pkts = shard.sum_over_ranks(env, float(count))
+    per_launch = sorted(s.elapsed_time(e) / 1e3 for s, e in zip(ev_s, ev_e))
+    launch_s = per_launch[len(per_launch) // 2] if args.steps % 2 else \
+        (per_launch[args.steps // 2 - 1] + per_launch[args.steps // 2]) / 2
+    b2b_s = ev_s[0].elapsed_time(ev_e[-1]) / 1e3 / args.steps
+    ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), t1 - t0, launch_s])
+    total_bytes = sum(r[0] for r in ranks)
+    total_pkts = sum(r[1] for r in ranks)
 
     gib_s = total_bytes * args.steps / elapsed / 2**30
     # L4 payload only: the checksummed bytes minus the TCP (20 B) /
@@ -145,15 +195,20 @@ def main() -> int:
         "dtype": "u8",
         "data": "synthetic: device-generated counter-hash packets (0.1% all-zero, 0.1% all-0xFF), 1024 flows",
         "config": {
-            "workload": f"{w.name}: {w.description}",
+            "workload": f"{w.name}: {w.describe(int(total_pkts), env.world)}",
             "packets_per_gpu": count,
-            "global_packets": n_total,
+            "global_packets": int(total_pkts),
             "l4_bytes_per_packet": w.length,
             "arena_stride": w.stride,
-            "parallelism": f"{env.world} shard(s), contiguous packet ranges, no data-path collective",
+            "parallelism": f"{env.world} shard(s), contiguous packet ranges"
+                           f"{' of equal bytes' if w.ragged else ''}, no data-path collective",
         },
         "mpkt_per_s": round(mpkt_s, 2),
         "per_gpu_gib_per_s": round(gib_s / env.world, 2),
+        # each rank's own rate over its own wall time and shard
+        "per_rank_gib_per_s": [round(r[0] * args.steps / r[2] / 2**30, 2) for r in ranks],
+        "per_rank_packets": [int(r[1]) for r in ranks],
+        "devices_visible": n_dev,
         "l4_payload_gib_per_s": round(payload_gib_s, 2),
         "roofline": {
             "bound": "hbm",
@@ -163,12 +218,15 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "kernel_ms": round(launch_s * 1e3, 4),
+            "kernel_ms_b2b_mean": round(b2b_s * 1e3, 4),
+            "kernel_ms_min": round(per_launch[0] * 1e3, 4),
+            "timing": "median of per-dispatch HIP event pairs on the launch stream",
             "algorithmic_bytes_per_launch": algo_bytes,
         },
         "cpu_baseline": None,
     }
 
-    if env.rank == 0 and env.world == 1 and not args.no_cpu and not w.ragged:
+    if env.rank == 0 and env.world == 1 and not args.no_cpu:
         line["cpu_baseline"], line["host_end_to_end"] = cpu_legs(args, w, out, count, first)
 
     shard.barrier(env)
@@ -178,10 +236,22 @@ def main() -> int:
     return 0
 
 
+def _timed(run, threads, budget_s=3.0, max_reps=50):
+    """Repeat run(threads) for about budget_s; return (reps, seconds)."""
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        run(threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or reps >= max_reps:
+            return reps, el
+
+
 def cpu_legs(args, w, gpu_out, count, first):
     """pip's own checksum on the host cores over a bounded sample of the same
-    packets (checked bit-exact against the GPU results), plus the PCIe-inclusive
-    host -> device -> host rate of the same sample through pipck_host_checksum_fixed."""
+    packets (checked bit-exact against the GPU results), plus -- for fixed
+    strides -- the PCIe-inclusive host -> device -> host rate of the same sample
+    through pipck_host_checksum_fixed."""
     import ctypes as C
 
     import numpy as np
@@ -190,8 +260,37 @@ def cpu_legs(args, w, gpu_out, count, first):
     from pip_amd import _lib
 
     threads = host_threads()
-    n = args.cpu_sample or min(count, max(1, (2 << 30) // w.stride))  # ~2 GiB sample
     orc = Oracle()
+    kind = "reference" if Reference.available() else "port"
+    ref = Reference() if kind == "reference" else None
+    flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto) if w.family else b""
+    gpu = gpu_out.cpu().numpy().view(np.uint16)
+
+    if w.ragged:
+        n = args.cpu_sample or min(count, 1 << 21)  # ~2M Zipf packets, ~2 GB
+        arena, offs, lens = orc.gen_ragged_batch(w.seed, first, n, w.hdr, threads)
+        l4 = int(lens.astype(np.int64).sum())
+
+        def run(t):
+            if ref:
+                return ref.batch_ragged(arena, offs, lens, w.family, w.proto, flows, N_FLOWS, first, t)
+            return orc.batch_ragged(arena, offs, lens, w.family, w.proto, w.seed, N_FLOWS, first, t)
+
+        res = run(threads)  # warm + correctness
+        verified = bool(np.array_equal(res, gpu[:n]))
+        reps, el = _timed(run, threads)
+        t0 = time.perf_counter()
+        run(1)
+        st = l4 / (time.perf_counter() - t0) / 2**30
+        cpu = {"value": round(l4 * reps / el / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+               "sample": f"first {n} packets of the same Zipf workload ({l4 / 2**30:.2f} GiB of L4 bytes), "
+                         f"pip_inet_checksum per packet, {reps} timed passes on {threads} threads; "
+                         f"1 thread: {st:.3f} GiB/s",
+               "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified}
+        return cpu, {"value": None, "note": "host end-to-end is measured for fixed strides (pipck_host_checksum_fixed)"}
+
+    # fixed strides: cfg1's whole 1M-header batch is a 20 MB sample; others ~2 GiB
+    n = args.cpu_sample or min(count, max(1, (2 << 30) // w.stride))
     lib = _lib.load()
     pin = lib.pipck_host_alloc(n * w.stride)
     if not pin:
@@ -199,32 +298,18 @@ def cpu_legs(args, w, gpu_out, count, first):
     arena = np.ctypeslib.as_array((C.c_uint8 * (n * w.stride)).from_address(pin))
     try:
         orc.lib.ock_gen_fixed_batch(w.seed, first, n, w.length, w.hdr, C.c_void_p(pin), w.stride, threads)
-        flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto) if w.family else b""
-        if Reference.available():
-            ref, kind = Reference(), "reference"
 
-            def run(t):
+        def run(t):
+            if ref:
                 return ref.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, flows, N_FLOWS, first, t)
-        else:
-            kind = "port"
-
-            def run(t):
-                return orc.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, w.seed, N_FLOWS, first, t)
+            return orc.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, w.seed, N_FLOWS, first, t)
 
         res = run(threads)  # warm + correctness
-        gpu = gpu_out[:n].cpu().numpy().view(np.uint16)
-        verified = bool(np.array_equal(res, gpu))
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            run(threads)
-            reps += 1
-            el = time.perf_counter() - t0
-            if el > 3.0 or reps >= 50:
-                break
+        verified = bool(np.array_equal(res, gpu[:n]))
+        reps, el = _timed(run, threads)
         mt = n * w.length * reps / el / 2**30
-        t0 = time.perf_counter()
-        run(1)
-        st = n * w.length / (time.perf_counter() - t0) / 2**30
+        reps1, el1 = _timed(run, 1, budget_s=1.0, max_reps=20)
+        st = n * w.length * reps1 / el1 / 2**30
 
         # host end-to-end: pinned host batch -> H2D -> kernel -> D2H (PCIe-bound)
         ctx = C.c_void_p()
@@ -243,10 +328,13 @@ def cpu_legs(args, w, gpu_out, count, first):
     finally:
         del arena
         lib.pipck_host_free(pin)
+    what = "pip_ip_checksum" if not w.family else f"pip_inet{'6' if w.family == 6 else ''}_checksum"
     cpu = {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-           "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.2f} GiB), "
+           "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.3f} GiB), {what} per packet, "
                      f"{reps} timed passes on {threads} threads; 1 thread: {st:.3f} GiB/s",
-           "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified}
+           "single_core_gib_per_s": round(st, 3),
+           "mpkt_per_s": round(n * reps / el / 1e6, 2), "single_core_mpkt_per_s": round(n * reps1 / el1 / 1e6, 2),
+           "gpu_results_match": verified}
     e2e_d = {"value": round(e2e, 2), "unit": "GiB/s", "sample_packets": n, "pinned": True, "results_match": e2e_ok}
     return cpu, e2e_d
 

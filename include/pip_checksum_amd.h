@@ -40,11 +40,13 @@ uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, str
                                 struct in6_addr dst);
 
 // ---- deferred forms for a batched TX path ----
-// Queue a packet on this thread's TX queue instead of checksumming it now; the
-// chain's bytes are copied at call time.  pip_checksum_amd_flush() checksums
-// every queued packet on the GPU in one batch and stores htons(checksum) into
-// each csum_field (what pip_tcp_packet.cpp:132-133 / pip_udp.cpp:51,61 /
-// pip_netif.cpp:97 store), so it must run before those packets are output.
+// Queue a packet on this thread's TX queue instead of checksumming it now.
+// The chain's bytes are copied at call time -- unless this thread turned
+// zero-copy on (below): then segments in pinned memory are read at flush time.
+// pip_checksum_amd_flush() checksums every queued packet on the GPU in one
+// batch and stores htons(checksum) into each csum_field (what
+// pip_tcp_packet.cpp:132-133 / pip_udp.cpp:51,61 / pip_netif.cpp:97 store), so
+// it must run before those packets are output.
 void pip_inet_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src,
                                     struct in_addr dst, void* csum_field);
 void pip_inet6_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
@@ -58,5 +60,27 @@ void pip_checksum_amd_flush();
 // submit, complete or flush on this thread -- output them only after that.
 void pip_checksum_amd_submit();
 void pip_checksum_amd_complete();
+
+// Zero-copy for this thread's queue -- an explicit opt-in, off by default and
+// never switched on by the environment.  While on, every queued segment that
+// lies in pinned memory (pipck_host_alloc / pipck_host_register, include/pipck.h)
+// is NOT copied: the GPU reads it in place when its batch runs, so its bytes
+// must stay unchanged until the flush (or the complete/submit after its
+// submit) returns.  The queue keeps each such chain (shared_ptr) alive until
+// then, and the pinned range cannot be freed meanwhile (PIPCK_EBUSY).
+void pip_checksum_amd_zero_copy(bool on);
+
+// Capture mode for this thread: pip's UNCHANGED TX call sites become queue
+// entries.  While on, the three calls pip's TX path makes --
+//   pip_ip_checksum(hdr, len >= 20)            ip_sum  at hdr + 10  (pip_netif.cpp:94-97)
+//   pip_inet{,6}_checksum_buf(chain, TCP, ..)  th_sum  at head + 16 (pip_tcp_packet.cpp:128-133)
+//   pip_inet{,6}_checksum_buf(chain, UDP, ..)  uh_sum  at head + 6  (pip_udp.cpp:50-51, 60-61)
+// -- queue the packet with that field and return 0; pip then stores htons(0),
+// which the next flush (or complete) overwrites with htons(checksum), the bytes
+// pip's own build writes.  So the packets (their pip_buf chains, which
+// pip_netif::output4 hands to output_ip_data_callback) must be held by the
+// caller and output only after that flush.  Other calls compute at once.
+void pip_checksum_amd_capture(bool on);
+bool pip_checksum_amd_capturing();
 
 #endif

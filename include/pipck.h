@@ -42,6 +42,7 @@ extern "C" {
 #define PIPCK_EHIP       3   /* a HIP runtime call failed; see pipck_last_error() */
 #define PIPCK_ENODEV     4   /* no gfx950 device / HIP unavailable */
 #define PIPCK_ENOMEM     5
+#define PIPCK_EBUSY      6   /* a pinned range is still read in place by a queued TX batch */
 
 #define PIPCK_MAX_SEG_LEN 65535u
 
@@ -140,23 +141,6 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
                        uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
                        uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, void* stream);
 
-/* Launch-shape override for tuning; 0 = automatic everywhere (process-wide).
- * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
- * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
- * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9/13/17/25/33 =
- * ring-pipelined 2/4/8/12/16/24/32); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
- * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
- * fixed kernel, bit 3 = XCD-grouped task split, bit 4 = no packed-tile
- * addressing in the ragged kernel, bit 5 = 4-wave ragged blocks (default 1),
- * bit 6 = never the small-packet kernel (packets <= 64 B incl. chunk offset),
- * bit 7 = never the short-stride flat kernel (16-B-multiple strides < 1 KiB),
- * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bit 16 = no
- * lane-per-segment path for ragged tiles of tiny segments, bit 17 = never the
- * tiny-stride flat kernel (8-B-multiple strides <= 64 B with pseudo-headers or
- * RX verify; loads_per_lane 4/8/16 = its ring, bits 8..15 its rows per wave
- * task, default 4 and 12), bit 18 = that kernel without pseudo-headers too, bits 24..27 =
- * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2). */
-void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */
 #define PIPCK_HDR_NONE 0
@@ -164,7 +148,7 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
 #define PIPCK_HDR_UDP  2
 #define PIPCK_HDR_IPV4 3
 uint64_t pipck_cfg_seed(uint32_t cfg);
-/* packets [first_pkt, first_pkt+n) at d_arena + i*stride; bytes [len,stride) zeroed */
+/* packets [first_pkt, first_pkt+n) at d_arena + i*stride (any stride >= len); bytes [len,stride) zeroed */
 int pipck_gen_fixed(void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint64_t first_pkt,
                     uint64_t seed, uint32_t hdr_kind, void* stream);
 /* Zipf lengths 64..9000 for packets [first_pkt, first_pkt+n) -> d_len */
@@ -204,19 +188,23 @@ int pipck_host_sum(pipck_ctx* ctx, const pipck_hseg* segs, uint32_t nseg, uint32
 int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stride, uint32_t len,
                               uint64_t n_packets, int family, const void* h_flows, uint32_t n_flows,
                               uint64_t flow_origin, uint16_t* h_out);
-/* Per-packet path (pipck_host_sum): 0 = staged (H2D copy, kernel, D2H copy),
- * 1 = zero-copy (the kernel reads the pinned, coherent staging buffer and
- * writes the result to pinned host memory), 2 = auto (zero-copy up to 64 KiB
- * of staged bytes; the default).  Process-wide; the initial mode comes from
- * the environment variable PIPCK_HOST_ZERO_COPY (0/1/2). */
-void pipck_host_zero_copy(int mode);
+/* This context's per-packet path (pipck_host_sum): 0 = staged (H2D copy,
+ * kernel, D2H copy), 1 = zero-copy (the kernel reads the pinned, coherent
+ * staging buffer and writes the result to pinned host memory), 2 = auto
+ * (zero-copy up to 64 KiB of staged bytes).  A new context starts in the mode
+ * the environment variable PIPCK_HOST_ZERO_COPY (0/1/2) names, default 2.
+ * Either path computes the same result. */
+int pipck_ctx_zero_copy(pipck_ctx* ctx, int mode);
 void* pipck_host_alloc(size_t bytes);   /* pinned, coherent host memory (device-readable in place) */
 /* Pin an existing host range (a utun / socket buffer ring) so the GPU can read
  * it in place at the same address; PIPCK_EINVAL if the runtime maps it to a
  * different device address. */
 int pipck_host_register(void* p, size_t bytes);
+/* Both refuse (PIPCK_EBUSY, nothing released) while a TX queue holds segments
+ * of the range for an in-place read that has not completed; PIPCK_EINVAL for a
+ * pointer that does not start such a range. */
 int pipck_host_unregister(void* p);
-void  pipck_host_free(void* p);
+int pipck_host_free(void* p);
 
 /* ---- deferred TX queue -------------------------
  * pip checksums each segment synchronously while building it
@@ -247,12 +235,15 @@ int pipck_txq_add4_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8
                       uint32_t dst, void* csum_field);
 int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8_t proto, const uint8_t* src,
                       const uint8_t* dst, void* csum_field);
-/* Automatic zero-copy (off by default; on at creation when the environment sets
- * PIPCK_TXQ_AUTO_ZERO_COPY=1): pipck_txq_add4/add6 then read every segment that
- * lies in a pinned range in place and copy the others, so pinned segments follow
- * the zero-copy contract above (valid and unchanged until their batch
- * completes).  Lets callers that cannot choose the _zc forms -- pip's deferred
- * drop-in -- use pinned utun/socket buffers without a copy. */
+/* Automatic zero-copy, an explicit per-queue opt-in (off at creation; no
+ * environment variable turns it on): pipck_txq_add4/add6 then read every
+ * segment that lies in a pinned range in place and copy the others, so pinned
+ * segments follow the zero-copy contract above -- the GPU reads them at flush
+ * time, so they must stay valid and UNCHANGED until their batch completes.
+ * Lets callers that cannot choose the _zc forms -- pip's deferred drop-in,
+ * through pip_checksum_amd_zero_copy() -- use pinned utun/socket buffers
+ * without a copy.  Every in-place segment holds its pinned range until its
+ * batch completes (see pipck_host_free). */
 int pipck_txq_auto_zero_copy(pipck_txq* q, int on);
 /* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);

@@ -122,6 +122,9 @@ class Oracle(_Common):
         L.ock_batch_fixed.argtypes = [_p, _u64, _u32, _u64, _i32, _u8, _u64, _u32, _u64, _p, _i32]
         L.ock_batch_ragged.argtypes = [_p, _p, _p, _u64, _i32, _u8, _u64, _u32, _u64, _p, _i32]
         L.ock_gen_fixed_batch.argtypes = [_u64, _u64, _u64, _u32, _u32, _p, _u64, _i32]
+        L.ock_gen_ragged_layout.restype = _u64
+        L.ock_gen_ragged_layout.argtypes = [_u64, _u64, _u64, _p, _p]
+        L.ock_gen_ragged_fill.argtypes = [_u64, _u64, _u64, _u32, _p, _p, _p, _i32]
 
     # ---- generator twin
     def mix64(self, x: int) -> int:
@@ -167,18 +170,15 @@ class Oracle(_Common):
         self.lib.ock_gen_fixed_batch(seed, first, n, length, hdr, _np_ptr(arena), stride, threads)
         return arena
 
-    def gen_ragged_batch(self, seed: int, first: int, n: int, hdr: int):
-        lens = self.zipf_lengths(seed, first, n)
-        rounded = (lens.astype(np.uint64) + 15) & ~np.uint64(15)
-        offs = np.zeros(n, dtype=np.uint64)
-        if n > 1:
-            offs[1:] = np.cumsum(rounded[:-1])
-        arena = np.zeros(int(offs[-1] + rounded[-1]) if n else 16, dtype=np.uint8)
-        for i in range(n):
-            L = int(lens[i])
-            o = int(offs[i])
-            arena[o:o + L] = np.frombuffer(self.packet(seed, first + i, L, hdr), dtype=np.uint8)
-        return arena, offs, lens
+    def gen_ragged_batch(self, seed: int, first: int, n: int, hdr: int, threads: int = 1):
+        """Zipf batch in the device layout (offsets = prefix of lengths rounded to 16):
+        (arena, offsets, lens)."""
+        lens = np.zeros(max(n, 1), dtype=np.uint32)
+        offs = np.zeros(max(n, 1), dtype=np.uint64)
+        total = self.lib.ock_gen_ragged_layout(seed, first, n, _np_ptr(lens), _np_ptr(offs))
+        arena = np.zeros(max(int(total), 16), dtype=np.uint8)
+        self.lib.ock_gen_ragged_fill(seed, first, n, hdr, _np_ptr(lens), _np_ptr(offs), _np_ptr(arena), threads)
+        return arena, offs[:n], lens[:n]
 
     # ---- batch checksums
     def batch_fixed(self, arena: np.ndarray, stride: int, length: int, n: int, family: int, proto: int,
@@ -209,15 +209,14 @@ class Reference(_Common):
         self.lib = C.CDLL(os.fspath(REF_SO))
         _declare(self.lib, self.prefix)
         self.lib.ref_batch_fixed.argtypes = [_p, _u64, _u32, _u64, _i32, _u8, _p, _p, _u32, _u64, _p, _i32]
+        self.lib.ref_batch_ragged.argtypes = [_p, _p, _p, _u64, _i32, _u8, _p, _p, _u32, _u64, _p, _i32]
 
     @staticmethod
     def available() -> bool:
         return REF_SO.exists()
 
-    def batch_fixed(self, arena: np.ndarray, stride: int, length: int, n: int, family: int, proto: int,
-                    flows: bytes, n_flows: int, flow_origin: int = 0, threads: int = 1) -> np.ndarray:
-        """flows: pipck_flow4/6 records as produced by Oracle.flows_table."""
-        out = np.zeros(n, dtype=np.uint16)
+    @staticmethod
+    def _flow_arrays(family: int, flows: bytes, n_flows: int):
         rec = 12 if family == 4 else 36
         raw = np.frombuffer(flows, dtype=np.uint8).reshape(n_flows, rec) if family else None
         f4 = f6 = None
@@ -225,7 +224,26 @@ class Reference(_Common):
             f4 = np.ascontiguousarray(raw[:, :8]).view(np.uint32).reshape(-1).copy()
         elif family == 6:
             f6 = np.ascontiguousarray(raw[:, :32]).copy()
+        return f4, f6
+
+    def batch_fixed(self, arena: np.ndarray, stride: int, length: int, n: int, family: int, proto: int,
+                    flows: bytes, n_flows: int, flow_origin: int = 0, threads: int = 1) -> np.ndarray:
+        """flows: pipck_flow4/6 records as produced by Oracle.flows_table."""
+        out = np.zeros(n, dtype=np.uint16)
+        f4, f6 = self._flow_arrays(family, flows, n_flows)
         self.lib.ref_batch_fixed(_np_ptr(arena), stride, length, n, family, proto,
                                  None if f4 is None else _np_ptr(f4), None if f6 is None else _np_ptr(f6),
                                  max(n_flows, 1), flow_origin, _np_ptr(out), threads)
+        return out
+
+    def batch_ragged(self, arena: np.ndarray, offsets: np.ndarray, lens: np.ndarray, family: int, proto: int,
+                     flows: bytes, n_flows: int, flow_origin: int = 0, threads: int = 1) -> np.ndarray:
+        """pip_inet{,6}_checksum per packet of a ragged batch (pip_checksum.cpp:42-87)."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        out = np.zeros(len(lens), dtype=np.uint16)
+        f4, f6 = self._flow_arrays(family, flows, n_flows)
+        self.lib.ref_batch_ragged(_np_ptr(arena), _np_ptr(offsets), _np_ptr(lens), len(lens), family, proto,
+                                  None if f4 is None else _np_ptr(f4), None if f6 is None else _np_ptr(f6),
+                                  max(n_flows, 1), flow_origin, _np_ptr(out), threads)
         return out

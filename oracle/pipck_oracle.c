@@ -241,6 +241,15 @@ static void* gen_worker(void* arg) {
     return NULL;
 }
 
+static void* gen_ragged_worker(void* arg) {
+    job_t* j = (job_t*)arg;
+    for (uint64_t i = j->begin; i < j->end; i++) {
+        uint32_t len = j->lens[i];
+        ock_gen_packet(j->seed, j->flow_origin + i, len, j->hdr_kind, j->gen_arena + j->offsets[i], (len + 15u) & ~15u);
+    }
+    return NULL;
+}
+
 static void run_jobs(job_t* proto_job, uint64_t n, int threads, void* (*fn)(void*)) {
     if (threads < 1) threads = 1;
     if ((uint64_t)threads > n) threads = n ? (int)n : 1;
@@ -286,4 +295,23 @@ void ock_gen_fixed_batch(uint64_t seed, uint64_t first, uint64_t n, uint32_t len
     j.seed = seed; j.flow_origin = first; j.len = len; j.hdr_kind = hdr_kind;
     j.gen_arena = arena; j.stride = stride;
     run_jobs(&j, n, threads, gen_worker);
+}
+
+uint64_t ock_gen_ragged_layout(uint64_t seed, uint64_t first, uint64_t n, uint32_t* lens, uint64_t* offsets) {
+    uint64_t off = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        lens[i] = ock_zipf_len(seed, first + i);
+        offsets[i] = off;
+        off += (lens[i] + 15u) & ~15u;
+    }
+    return off;
+}
+
+void ock_gen_ragged_fill(uint64_t seed, uint64_t first, uint64_t n, uint32_t hdr_kind, const uint32_t* lens,
+                         const uint64_t* offsets, uint8_t* arena, int threads) {
+    job_t j;
+    memset(&j, 0, sizeof j);
+    j.seed = seed; j.flow_origin = first; j.hdr_kind = hdr_kind; j.lens = lens; j.offsets = offsets;
+    j.gen_arena = arena;
+    run_jobs(&j, n, threads, gen_ragged_worker);
 }

@@ -60,6 +60,12 @@ void ock_batch_ragged(const uint8_t* arena, const uint64_t* offsets, const uint3
 /* generate a fixed-stride batch of packets [first, first+n) into arena */
 void ock_gen_fixed_batch(uint64_t seed, uint64_t first, uint64_t n, uint32_t len, uint32_t hdr_kind,
                          uint8_t* arena, uint64_t stride, int threads);
+/* Zipf lengths of packets [first, first+n) and their offsets in the device layout
+ * (exclusive prefix of the lengths rounded up to 16); returns the arena size */
+uint64_t ock_gen_ragged_layout(uint64_t seed, uint64_t first, uint64_t n, uint32_t* lens, uint64_t* offsets);
+/* packets [first, first+n) at arena + offsets[i], lens[i] bytes each, padding to 16 zeroed */
+void ock_gen_ragged_fill(uint64_t seed, uint64_t first, uint64_t n, uint32_t hdr_kind, const uint32_t* lens,
+                         const uint64_t* offsets, uint8_t* arena, int threads);
 
 #ifdef __cplusplus
 }

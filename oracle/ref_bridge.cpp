@@ -97,4 +97,35 @@ void ref_batch_fixed(const uint8_t* arena, uint64_t stride, uint32_t len, uint64
     for (auto& x : th) x.join();
 }
 
+// The same over a ragged batch: packet i at arena + offsets[i], lens[i] bytes,
+// through pip_inet_checksum (pip_checksum.cpp:42-61) / pip_inet6_checksum (:63-87).
+void ref_batch_ragged(const uint8_t* arena, const uint64_t* offsets, const uint32_t* lens, uint64_t n, int family,
+                      uint8_t proto, const uint32_t* flows4, const uint8_t* flows6, uint32_t n_flows,
+                      uint64_t flow_origin, uint16_t* out, int threads) {
+    if (threads < 1) threads = 1;
+    auto work = [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            const uint8_t* p = arena + offsets[i];
+            const uint32_t f = (uint32_t)((flow_origin + i) % n_flows);
+            if (family == 4) {
+                pip_in_addr s, d;
+                s.s_addr = flows4[2 * f];
+                d.s_addr = flows4[2 * f + 1];
+                out[i] = pip_inet_checksum(p, proto, s, d, (pip_uint16)lens[i]);
+            } else if (family == 6) {
+                pip_in6_addr s, d;
+                std::memcpy(&s, flows6 + 32 * f, 16);
+                std::memcpy(&d, flows6 + 32 * f + 16, 16);
+                out[i] = pip_inet6_checksum(p, proto, s, d, (pip_uint16)lens[i]);
+            } else {
+                out[i] = pip_ip_checksum(p, lens[i]);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, n * t / threads, n * (t + 1) / threads);
+    work(0, n / threads);
+    for (auto& x : th) x.join();
+}
+
 }  // extern "C"

@@ -9,6 +9,11 @@
 // pip_checksum symbols at the call sites pip/pip_netif.cpp:97,
 // pip/protocol/pip_udp.cpp:50,60 and pip/protocol/pip_tcp_packet.cpp:128,130.
 // Each emitted packet is also re-verified with an independent RFC 1071 sum.
+// The _amd driver with PIPCK_REPLAY_CAPTURE=1 runs the same script with the
+// drop-in's capture mode on (pip_checksum_amd_capture): pip's unchanged call
+// sites queue their checksums, the output callback holds each packet's
+// segments, and after every stack action one flush stores all fields before
+// the packets are emitted -- the output must still equal pip's own build.
 #include "pip_netif.h"
 #include "pip_checksum.h"
 #include "protocol/pip_tcp.h"
@@ -19,16 +24,45 @@
 #include <string>
 #include <vector>
 
+#ifdef PIPCK_DEFERRED_CHECK
+#include "pip_checksum_amd.h"
+#include "pipck.h"
+#endif
+
 static std::vector<std::vector<uint8_t>> g_out;
 static std::shared_ptr<pip_tcp> g_tcp;
+static bool g_capture = false;
+// capture mode: packets whose checksum fields the next flush fills, as segment lists
+// (pip_netif::output4 unlinks its IPv4 header from the chain after the callback)
+static std::vector<std::vector<std::shared_ptr<pip_buf>>> g_pending;
 
-static void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
+static void emit(const std::vector<std::shared_ptr<pip_buf>>& segs) {
     std::vector<uint8_t> pkt;
-    for (auto q = buf; q; q = q->next()) {
+    for (auto& q : segs) {
         auto* p = (const uint8_t*)q->payload();
         pkt.insert(pkt.end(), p, p + q->payload_len());
     }
     g_out.push_back(pkt);
+}
+
+static void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
+    std::vector<std::shared_ptr<pip_buf>> segs;
+    for (auto q = buf; q; q = q->next()) segs.push_back(q);
+    if (g_capture)
+        g_pending.push_back(std::move(segs));
+    else
+        emit(segs);
+}
+
+// After each stack action: in capture mode, one flush fills every queued field,
+// then the held packets go out in order.
+static void settle() {
+#ifdef PIPCK_DEFERRED_CHECK
+    if (!g_capture) return;
+    pip_checksum_amd_flush();
+    for (auto& segs : g_pending) emit(segs);
+    g_pending.clear();
+#endif
 }
 
 static void on_connect(pip_netif&, std::shared_ptr<pip_tcp> tcp, const void* hs, pip_uint16) {
@@ -124,34 +158,40 @@ static void tcp_session(const Peer& pe, uint16_t mss, uint32_t write_len) {
     uint32_t cseq = 1000;
     auto syn = craft_tcp(pe, cseq, 0, TH_SYN, 65535, opts, {});
     pip_netif::shared().input(syn.data());
+    settle();
     if (!g_tcp) { printf("ERR no connection\n"); return; }
     uint32_t sseq = last_seq_from_server(pe) + 1;
     cseq += 1;
     auto ack = craft_tcp(pe, cseq, sseq, TH_ACK, 65535, {}, {});
     pip_netif::shared().input(ack.data());
+    settle();
 
     std::vector<uint8_t> payload(write_len);
     for (uint32_t i = 0; i < write_len; i++) payload[i] = (uint8_t)(i * 7 + 3);
     uint32_t w = g_tcp->write(payload.data(), write_len, true);
+    settle();
     sseq += w;
     // client acks everything and sends 101 odd bytes of data
     std::vector<uint8_t> cdata(101);
     for (size_t i = 0; i < cdata.size(); i++) cdata[i] = (uint8_t)(0xF0 ^ i);
     auto dat = craft_tcp(pe, cseq, sseq, TH_ACK | TH_PUSH, 65535, {}, cdata);
     pip_netif::shared().input(dat.data());
+    settle();
     cseq += (uint32_t)cdata.size();
     g_tcp->received((pip_uint16)cdata.size());
+    settle();
     // a 1-byte write, acked, then close
     uint8_t one = 0xAB;
     sseq += g_tcp->write(&one, 1, true);
+    settle();
     auto ack2 = craft_tcp(pe, cseq, sseq, TH_ACK, 65535, {}, {});
     pip_netif::shared().input(ack2.data());
+    settle();
     g_tcp->close();
+    settle();
 }
 
 #ifdef PIPCK_DEFERRED_CHECK
-#include "pip_checksum_amd.h"
-
 // The deferred (batched) TX API of libpip_checksum_amd.so on real pip_buf
 // chains built by pip's own pip_buf class: every emitted IPv4 header and
 // TCP/UDP segment is rebuilt as a chain (header with its checksum zeroed ->
@@ -230,6 +270,67 @@ static void deferred_check(bool pipelined) {
     fprintf(stderr, "DEFERRED mode %s queued %llu checked %zu bad %d pending_after %llu\n",
             pipelined ? "pipelined" : "flush", pending, k, bad, (unsigned long long)pip_checksum_amd_pending());
 }
+
+// Zero-copy through the drop-in (pip_checksum_amd_zero_copy): every TCP/UDP
+// segment pip emitted is rebuilt as a pip_buf chain whose header and payload
+// live in pinned memory (pipck_host_alloc) and are read by the GPU at flush
+// time.  The caller drops every reference to the chains before the flush --
+// the drop-in keeps them alive -- and freeing the pinned pool while the batch
+// is queued is refused (PIPCK_EBUSY); after the flush it succeeds.
+static void deferred_check_zero_copy() {
+    const size_t cap = 1 << 20;
+    uint8_t* pool = (uint8_t*)pipck_host_alloc(cap);
+    if (!pool) {
+        fprintf(stderr, "DEFERRED mode zero_copy pipck_host_alloc failed\n");
+        return;
+    }
+    pip_checksum_amd_zero_copy(true);
+    struct Item {
+        uint8_t field[2];
+        uint16_t wire;
+    };
+    std::vector<Item> items(g_out.size());
+    size_t k = 0, pos = 0;
+    for (auto& pk : g_out) {
+        const int ver = pk[0] >> 4;
+        const size_t hl = ver == 4 ? 20 : 40;
+        const uint8_t proto = ver == 4 ? pk[9] : pk[6];
+        const size_t csum_off = proto == IPPROTO_TCP ? 16 : 6;
+        const size_t l4h = proto == IPPROTO_TCP ? (pk[hl + 12] >> 4) * 4 : 8;
+        const size_t l4 = pk.size() - hl;
+        if (pos + l4 + 32 > cap) break;
+        uint8_t* hdr = pool + pos;
+        memcpy(hdr, &pk[hl], l4);
+        hdr[csum_off] = hdr[csum_off + 1] = 0;
+        pos = (pos + l4 + 15) & ~(size_t)15;
+        auto head = std::make_shared<pip_buf>(hdr, (pip_uint32)l4h, 0);
+        if (l4 > l4h) head->set_next(std::make_shared<pip_buf>(hdr + l4h, (pip_uint32)(l4 - l4h), 0));
+        Item& it = items[k++];
+        if (ver == 4) {
+            struct in_addr s, d;
+            memcpy(&s, &pk[12], 4);
+            memcpy(&d, &pk[16], 4);
+            it.wire = pip_inet_checksum_buf(head, proto, s, d);
+            pip_inet_checksum_buf_deferred(head, proto, s, d, it.field);
+        } else {
+            struct in6_addr s6, d6;
+            memcpy(&s6, &pk[8], 16);
+            memcpy(&d6, &pk[24], 16);
+            it.wire = pip_inet6_checksum_buf(head, proto, s6, d6);
+            pip_inet6_checksum_buf_deferred(head, proto, s6, d6, it.field);
+        }
+    }  // every chain reference of this function is gone here
+    const unsigned long long pending = pip_checksum_amd_pending();
+    const int busy = pipck_host_free(pool);
+    pip_checksum_amd_flush();
+    int bad = 0;
+    for (size_t i = 0; i < k; i++)
+        if ((uint16_t)(items[i].field[0] << 8 | items[i].field[1]) != items[i].wire) bad++;
+    const int freed = pipck_host_free(pool);
+    pip_checksum_amd_zero_copy(false);
+    fprintf(stderr, "DEFERRED mode zero_copy queued %llu checked %zu bad %d pending_after %llu free_while_queued %d "
+            "free_after %d\n", pending, k, bad, (unsigned long long)pip_checksum_amd_pending(), busy, freed);
+}
 #endif
 
 int main() {
@@ -238,6 +339,12 @@ int main() {
     uint8_t z[20] = {0};
     (void)pip_ip_checksum(z, 20);
 
+#ifdef PIPCK_DEFERRED_CHECK
+    if (getenv("PIPCK_REPLAY_CAPTURE")) {
+        pip_checksum_amd_capture(true);
+        g_capture = true;
+    }
+#endif
     auto& nif = pip_netif::shared();
     nif.output_ip_data_callback = on_output;
     nif.new_tcp_connect_callback = on_connect;
@@ -256,10 +363,12 @@ int main() {
         pip_udp::output(buf.data(), n, "10.0.0.1", 5353, "10.0.0.2", 53);
         pip_udp::output(buf.data(), n, "fd00::1", 5353, "fd00::2", 53);
     }
+    settle();  // one flush for all 14 datagrams (their payload is still intact)
     // an all-0xFF and an all-zero UDP payload exercise the 0x0000 / 0xFFFF edge
     std::vector<uint8_t> ff(64, 0xFF), zz(64, 0);
     pip_udp::output(ff.data(), 64, "255.255.255.255", 65535, "255.255.255.255", 65535);
     pip_udp::output(zz.data(), 64, "0.0.0.0", 0, "0.0.0.0", 0);
+    settle();
 
     int bad = 0;
     for (auto& pk : g_out) {
@@ -269,8 +378,11 @@ int main() {
     }
     printf("PACKETS %zu VERIFY_BAD %d\n", g_out.size(), bad);
 #ifdef PIPCK_DEFERRED_CHECK
+    pip_checksum_amd_capture(false);
+    g_capture = false;
     deferred_check(false);
     deferred_check(true);
+    deferred_check_zero_copy();
 #endif
     fflush(stdout);
     _exit(0);  // pip's timer thread is detached and never stops

@@ -18,7 +18,7 @@ LIB_DIR = Path(__file__).resolve().parent / "lib"
 LIBPIPCK = Path(os.environ.get("PIPCK_LIB") or LIB_DIR / "libpipck.so")
 LIBSHIM = LIB_DIR / "libpip_checksum_amd.so"
 
-PIPCK_OK, PIPCK_EINVAL, PIPCK_ERANGE, PIPCK_EHIP, PIPCK_ENODEV, PIPCK_ENOMEM = range(6)
+PIPCK_OK, PIPCK_EINVAL, PIPCK_ERANGE, PIPCK_EHIP, PIPCK_ENODEV, PIPCK_ENOMEM, PIPCK_EBUSY = range(7)
 MAX_SEG_LEN = 65535
 HDR_NONE, HDR_TCP, HDR_UDP, HDR_IPV4 = 0, 1, 2, 3
 
@@ -55,7 +55,6 @@ SIGNATURES = {
     "pipck_verify_ragged": (_i32, [_p, _p, _u64, _p, _p, _p, _p]),
     "pipck_update_fixed": (_i32, [_p, _u64, _u64, _u32, _u32, _u32, _u32, _u32, _p, _u64, _p, _p, _u32, _p, _u64,
                                   _p]),
-    "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
     "pipck_cfg_seed": (_u64, [_u32]),
     "pipck_gen_fixed": (_i32, [_p, _u64, _u32, _u64, _u64, _u64, _u32, _p]),
     "pipck_gen_zipf_lengths": (_i32, [_p, _u64, _u64, _u64, _p]),
@@ -68,7 +67,7 @@ SIGNATURES = {
     "pipck_host_sum": (_i32, [_p, C.POINTER(HSeg), _u32, _u32, C.POINTER(_u32)]),
     "pipck_host_checksum_fixed": (_i32, [_p, _p, _u64, _u32, _u64, _i32, _p, _u32, _u64, _p]),
     "pipck_host_alloc": (_p, [_sz]),
-    "pipck_host_free": (None, [_p]),
+    "pipck_host_free": (_i32, [_p]),
     "pipck_txq_create": (_i32, [_p, C.POINTER(_p)]),
     "pipck_txq_destroy": (_i32, [_p]),
     "pipck_txq_add4": (_i32, [_p, C.POINTER(HSeg), _u32, _u8, _u32, _u32, _p]),
@@ -80,11 +79,16 @@ SIGNATURES = {
     "pipck_host_unregister": (_i32, [_p]),
     "pipck_txq_pending": (_u64, [_p]),
     "pipck_txq_flush": (_i32, [_p]),
-    "pipck_host_zero_copy": (None, [_i32]),
+    "pipck_ctx_zero_copy": (_i32, [_p, _i32]),
     "pipck_txq_submit": (_i32, [_p]),
     "pipck_txq_complete": (_i32, [_p]),
     "pipck_txq_inflight": (_u64, [_p]),
     "pipck_txq_auto_zero_copy": (_i32, [_p, _i32]),
+}
+
+# the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only
+INTERNAL_SIGNATURES = {
+    "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
 }
 
 _lib = None
@@ -106,7 +110,7 @@ def load() -> C.CDLL:
             f"{LIBPIPCK} is missing: build it with `make -C {LIB_DIR.parent}` "
             "(or __graft_entry__.build()); there is no CPU fallback")
     lib = C.CDLL(os.fspath(LIBPIPCK), mode=C.RTLD_GLOBAL)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in {**SIGNATURES, **INTERNAL_SIGNATURES}.items():
         if os.environ.get("PIPCK_LIB") and not hasattr(lib, name):
             continue  # an older build under A/B may predate some entry points
         fn = getattr(lib, name)

@@ -27,6 +27,11 @@ def _ctx() -> C.c_void_p:
     return ctx
 
 
+def set_zero_copy(mode: int) -> None:
+    """This thread's per-packet path: 0 staged, 1 zero-copy, 2 auto (pipck_ctx_zero_copy)."""
+    call("pipck_ctx_zero_copy", _ctx(), mode)
+
+
 def _device_sum(segments: Sequence[bytes], init: int) -> int:
     bufs = [C.create_string_buffer(bytes(s), max(len(s), 1)) for s in segments]
     arr = (HSeg * max(len(segments), 1))()

@@ -8,9 +8,12 @@
 // pipck_host_sum(), which replays pip's per-segment loop on the device.
 // Contexts are per thread (thread_local), so calls stay reentrant and
 // lock-free across pip's TX threads, as pip's own functions are.
+#include <netinet/in.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "../../include/pip_buf_layout.h"
 #include "../../include/pip_checksum_amd.h"
@@ -26,8 +29,16 @@ namespace {
 struct ThreadCtx {
     pipck_ctx* ctx = nullptr;
     pipck_txq* txq = nullptr;
+    bool zero_copy = false;  // pip_checksum_amd_zero_copy(): pinned segments read in place at flush
+    bool capture = false;    // pip_checksum_amd_capture(): pip's TX calls queue instead of computing
+    // Chains whose pinned segments a batch reads in place stay referenced until
+    // that batch completes (pip may drop its own references before the flush):
+    // `keep` for the batch receiving adds, `keep_inflight` for the submitted one.
+    std::vector<std::shared_ptr<pip_buf>> keep, keep_inflight;
     ~ThreadCtx() {
-        if (txq) pipck_txq_destroy(txq);
+        if (txq) pipck_txq_destroy(txq);  // waits for the in-flight batch
+        keep.clear();
+        keep_inflight.clear();
         if (ctx) pipck_ctx_destroy(ctx);
     }
     pipck_ctx* get() {
@@ -95,6 +106,10 @@ struct ChainSegs {
     ChainSegs& operator=(const ChainSegs&) = delete;
 };
 
+void queue_chain(const std::shared_ptr<pip_buf>& buf, uint8_t proto, const void* src, const void* dst, int family,
+                 void* csum_field);
+uint8_t* capture_field(const std::shared_ptr<pip_buf>& buf, uint8_t proto);
+
 uint16_t chain_checksum(const std::shared_ptr<pip_buf>& buf, uint32_t pseudo) {
     ChainSegs c(buf);
     // length term: the head's u32 total_len split hi + lo (pip_checksum.cpp:140-142)
@@ -112,6 +127,10 @@ uint32_t pip_standard_checksum(const void* payload, uint32_t len, uint32_t sum) 
 }
 
 uint16_t pip_ip_checksum(const void* payload, uint32_t len) {
+    if (t_ctx.capture && payload && len >= 20) {  // ip_sum at byte 10 (pip/pip_netif.cpp:94-97)
+        pip_ip_checksum_deferred(payload, len, (uint8_t*)payload + 10);
+        return 0;  // the caller stores htons(0); the flush stores the checksum over it
+    }
     return (uint16_t)~(uint16_t)pip_standard_checksum(payload, len, 0);
 }
 
@@ -128,11 +147,21 @@ uint16_t pip_inet6_checksum(const void* payload, uint8_t proto, struct in6_addr 
 }
 
 uint16_t pip_inet_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src, struct in_addr dst) {
+    if (t_ctx.capture)
+        if (uint8_t* field = capture_field(buf, proto)) {
+            queue_chain(buf, proto, &src.s_addr, &dst.s_addr, 4, field);
+            return 0;  // the caller stores htons(0); the flush stores the checksum over it
+        }
     return chain_checksum(buf, v4_terms(src) + v4_terms(dst) + proto);
 }
 
 uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
                                 struct in6_addr dst) {
+    if (t_ctx.capture)
+        if (uint8_t* field = capture_field(buf, proto)) {
+            queue_chain(buf, proto, src.s6_addr, dst.s6_addr, 6, field);
+            return 0;
+        }
     return chain_checksum(buf, v6_terms(src) + v6_terms(dst) + proto);
 }
 
@@ -140,18 +169,41 @@ uint16_t pip_inet6_checksum_buf(std::shared_ptr<pip_buf> buf, uint8_t proto, str
 // The queue computes the pseudo-header from the addresses itself and takes the
 // length term from the queued bytes, which for a pip_buf chain equals the
 // head's total_len (pip/pip_buf.h:81-97 keeps it as the sum of the segments).
+namespace {
+
+void queue_chain(const std::shared_ptr<pip_buf>& buf, uint8_t proto, const void* src, const void* dst, int family,
+                 void* csum_field) {
+    ChainSegs c(buf);
+    pipck_txq* q = t_ctx.queue();
+    int rc = family == 4 ? pipck_txq_add4(q, c.segs, c.n, proto, *(const uint32_t*)src, *(const uint32_t*)dst,
+                                          csum_field)
+                         : pipck_txq_add6(q, c.segs, c.n, proto, (const uint8_t*)src, (const uint8_t*)dst, csum_field);
+    if (rc) die(family == 4 ? "pipck_txq_add4" : "pipck_txq_add6", rc);
+    if (t_ctx.zero_copy) t_ctx.keep.push_back(buf);  // its pinned segments are read at flush time
+}
+
+// Where pip's TX callers store a chain's checksum: th_sum at byte 16 of the TCP
+// header segment (pip/protocol/pip_tcp_packet.cpp:132-133), uh_sum at byte 6
+// of the UDP header segment (pip/protocol/pip_udp.cpp:50-51, 60-61); null for
+// anything else (computed synchronously even in capture mode).
+uint8_t* capture_field(const std::shared_ptr<pip_buf>& buf, uint8_t proto) {
+    const pip_buf_layout* head = reinterpret_cast<const pip_buf_layout*>(buf.get());
+    if (!head || !head->payload) return nullptr;
+    if (proto == IPPROTO_TCP && head->payload_len >= 20) return (uint8_t*)head->payload + 16;
+    if (proto == IPPROTO_UDP && head->payload_len >= 8) return (uint8_t*)head->payload + 6;
+    return nullptr;
+}
+
+}  // namespace
+
 void pip_inet_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in_addr src,
                                     struct in_addr dst, void* csum_field) {
-    ChainSegs c(buf);
-    int rc = pipck_txq_add4(t_ctx.queue(), c.segs, c.n, proto, src.s_addr, dst.s_addr, csum_field);
-    if (rc) die("pipck_txq_add4", rc);
+    queue_chain(buf, proto, &src.s_addr, &dst.s_addr, 4, csum_field);
 }
 
 void pip_inet6_checksum_buf_deferred(std::shared_ptr<pip_buf> buf, uint8_t proto, struct in6_addr src,
                                      struct in6_addr dst, void* csum_field) {
-    ChainSegs c(buf);
-    int rc = pipck_txq_add6(t_ctx.queue(), c.segs, c.n, proto, src.s6_addr, dst.s6_addr, csum_field);
-    if (rc) die("pipck_txq_add6", rc);
+    queue_chain(buf, proto, src.s6_addr, dst.s6_addr, 6, csum_field);
 }
 
 void pip_ip_checksum_deferred(const void* hdr, uint32_t len, void* csum_field) {
@@ -161,17 +213,31 @@ void pip_ip_checksum_deferred(const void* hdr, uint32_t len, void* csum_field) {
 
 uint64_t pip_checksum_amd_pending() { return pipck_txq_pending(t_ctx.queue()); }
 
-void pip_checksum_amd_flush() {
-    int rc = pipck_txq_flush(t_ctx.queue());
-    if (rc) die("pipck_txq_flush", rc);
-}
-
 void pip_checksum_amd_submit() {
     int rc = pipck_txq_submit(t_ctx.queue());
     if (rc) die("pipck_txq_submit", rc);
+    // the batch submitted before this one has completed; this one is in flight now
+    t_ctx.keep_inflight.clear();
+    t_ctx.keep_inflight.swap(t_ctx.keep);
 }
 
 void pip_checksum_amd_complete() {
     int rc = pipck_txq_complete(t_ctx.queue());
     if (rc) die("pipck_txq_complete", rc);
+    t_ctx.keep_inflight.clear();
 }
+
+void pip_checksum_amd_flush() {
+    pip_checksum_amd_submit();
+    pip_checksum_amd_complete();
+}
+
+void pip_checksum_amd_zero_copy(bool on) {
+    int rc = pipck_txq_auto_zero_copy(t_ctx.queue(), on ? 1 : 0);
+    if (rc) die("pipck_txq_auto_zero_copy", rc);
+    t_ctx.zero_copy = on;
+}
+
+void pip_checksum_amd_capture(bool on) { t_ctx.capture = on; }
+
+bool pip_checksum_amd_capturing() { return t_ctx.capture; }

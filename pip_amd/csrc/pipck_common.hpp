@@ -3,9 +3,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+#include <memory>
 #include <string>
 
 #include "../../include/pipck.h"
+#include "pipck_testing.h"
 
 namespace pipck {
 
@@ -38,17 +41,26 @@ int device_cus();
 // Registry of the pinned host ranges the GPU may read in place (made by
 // pipck_host_alloc / pipck_host_register).  Zero-copy TX segments are checked
 // against it at add time: a kernel touching an unpinned host page would fault
-// the GPU, so a bad pointer must fail as PIPCK_EINVAL instead.
-struct PinnedRange {
+// the GPU, so a bad pointer must fail as PIPCK_EINVAL instead.  A queue that
+// records a segment for an in-place read also HOLDS the segment's range until
+// that batch completes: pipck_host_free / pipck_host_unregister refuse a held
+// range (PIPCK_EBUSY), so no range can be released while the GPU may read it.
+struct PinnedRec {
     uintptr_t lo = 0, hi = 0;  // [lo, hi)
+    // holders in the low bits, kPinnedRemoved once released: one atomic word,
+    // so "acquire unless removed" and "remove unless held" cannot interleave
+    std::atomic<uint64_t> state{0};
 };
+constexpr uint64_t kPinnedRemoved = 1ull << 63;
+using PinnedRef = std::shared_ptr<PinnedRec>;
 void pinned_add(const void* p, size_t bytes);
-void pinned_remove(const void* p);
-// true if [p, p+len) lies inside one registered range; *hit returns that range
-bool pinned_lookup(const void* p, size_t len, PinnedRange* hit);
-// Changes whenever a range is removed: callers caching ranges drop their cache
-// then, so a freed (and perhaps reused, unpinned) buffer is never read in place.
-uint64_t pinned_generation();
+// PIPCK_OK, PIPCK_EINVAL (not a range start) or PIPCK_EBUSY (held by a queued batch)
+int pinned_remove(const void* p);
+// The range holding all of [p, p+len), or null.
+PinnedRef pinned_lookup(const void* p, size_t len);
+// Take / drop one hold; acquire fails once the range has been removed.
+bool pinned_acquire(PinnedRec& r);
+void pinned_release(PinnedRec& r);
 
 // pipck_checksum_chains without argument checks, for callers whose segment
 // descriptors hold absolute device-accessible addresses (d_arena == nullptr):

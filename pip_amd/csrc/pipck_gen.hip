@@ -78,6 +78,19 @@ __global__ __launch_bounds__(256) void k_gen_fixed(uint64_t* __restrict__ arena,
     }
 }
 
+// Byte strides (cfg1's packed 20-B headers): one lane per byte of the slot.
+__global__ __launch_bounds__(256) void k_gen_fixed_bytes(uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
+                                                         uint64_t n, uint64_t first, uint64_t seed, uint32_t hdr) {
+    const uint64_t total = n * stride;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
+         b += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = b / stride;
+        const uint32_t k = (uint32_t)(b - i * stride);
+        const uint64_t key = pkt_key(seed, first + i);
+        arena[b] = (uint8_t)(packet_word(key, packet_class(key), len, hdr, k / 8) >> (8 * (k % 8)));
+    }
+}
+
 __global__ void k_gen_zipf(uint32_t* __restrict__ out, uint64_t n, uint64_t first, uint64_t seed,
                            const uint64_t* __restrict__ cum, uint32_t K) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -176,9 +189,15 @@ uint64_t pipck_cfg_seed(uint32_t cfg) { return 0x9E3779B97F4A7C15ull ^ (uint64_t
 int pipck_gen_fixed(void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint64_t first_pkt, uint64_t seed,
                     uint32_t hdr_kind, void* stream) {
     if (!n) return PIPCK_OK;
-    if (!d_arena || stride % 8 || (uintptr_t)d_arena % 8 || stride < len) {
-        set_error("pipck_gen_fixed: arena and stride must be 8-byte aligned and stride >= len");
+    if (!d_arena || stride < len || stride == 0) {
+        set_error("pipck_gen_fixed: null arena or stride < len");
         return PIPCK_EINVAL;
+    }
+    if (stride % 8 || (uintptr_t)d_arena % 8) {
+        hipLaunchKernelGGL(k_gen_fixed_bytes, dim3(gen_grid((n * stride + 63) / 64)), dim3(256), 0, as_stream(stream),
+                           (uint8_t*)d_arena, stride, len, n, first_pkt, seed, hdr_kind);
+        PIPCK_LAUNCHED("k_gen_fixed_bytes");
+        return PIPCK_OK;
     }
     hipLaunchKernelGGL(k_gen_fixed, dim3(gen_grid(n)), dim3(256), 0, as_stream(stream), (uint64_t*)d_arena, stride / 8,
                        len, n, first_pkt, seed, hdr_kind);

@@ -24,43 +24,58 @@
 namespace pipck {
 
 static thread_local std::string t_err;
-// pipck_host_sum path: staged copies (0), zero-copy host access (1), or
-// auto (2: zero-copy up to kZeroCopyMax staged bytes); initial value from
-// PIPCK_HOST_ZERO_COPY, default auto.
-static std::atomic<int> g_zero_copy{[] {
+// pipck_host_sum path of a new context: staged copies (0), zero-copy host
+// access (1), or auto (2: zero-copy up to kZeroCopyMax staged bytes); from
+// PIPCK_HOST_ZERO_COPY at creation, default auto; per context afterwards
+// (pipck_ctx_zero_copy).
+static int default_zero_copy() {
     const char* e = getenv("PIPCK_HOST_ZERO_COPY");
     return e && (*e == '0' || *e == '1') ? *e - '0' : 2;
-}()};
+}
 constexpr size_t kZeroCopyMax = 64u << 10;
 void set_error(const std::string& msg) { t_err = msg; }
 
 static std::shared_mutex g_pinned_mu;
-static std::map<uintptr_t, uintptr_t> g_pinned;  // lo -> hi
-static std::atomic<uint64_t> g_pinned_gen{0};     // bumped by every removal
-
-uint64_t pinned_generation() { return g_pinned_gen.load(std::memory_order_acquire); }
+static std::map<uintptr_t, PinnedRef> g_pinned;  // lo -> range
 
 void pinned_add(const void* p, size_t bytes) {
+    auto r = std::make_shared<PinnedRec>();
+    r->lo = (uintptr_t)p;
+    r->hi = (uintptr_t)p + bytes;
     std::unique_lock<std::shared_mutex> g(g_pinned_mu);
-    g_pinned[(uintptr_t)p] = (uintptr_t)p + bytes;
+    g_pinned[(uintptr_t)p] = std::move(r);
 }
 
-void pinned_remove(const void* p) {
+int pinned_remove(const void* p) {
     std::unique_lock<std::shared_mutex> g(g_pinned_mu);
-    g_pinned.erase((uintptr_t)p);
-    g_pinned_gen.fetch_add(1, std::memory_order_acq_rel);
+    auto it = g_pinned.find((uintptr_t)p);
+    if (it == g_pinned.end()) return PIPCK_EINVAL;
+    uint64_t expect = 0;
+    if (!it->second->state.compare_exchange_strong(expect, kPinnedRemoved, std::memory_order_acq_rel))
+        return PIPCK_EBUSY;  // a queued batch will read it in place
+    g_pinned.erase(it);
+    return PIPCK_OK;
 }
 
-bool pinned_lookup(const void* p, size_t len, PinnedRange* hit) {
+PinnedRef pinned_lookup(const void* p, size_t len) {
     const uintptr_t a = (uintptr_t)p;
     std::shared_lock<std::shared_mutex> g(g_pinned_mu);
     auto it = g_pinned.upper_bound(a);
-    if (it == g_pinned.begin()) return false;
+    if (it == g_pinned.begin()) return nullptr;
     --it;
-    if (a + len > it->second) return false;
-    if (hit) *hit = PinnedRange{it->first, it->second};
+    if (a + len > it->second->hi) return nullptr;
+    return it->second;
+}
+
+bool pinned_acquire(PinnedRec& r) {
+    uint64_t s = r.state.load(std::memory_order_acquire);
+    do {
+        if (s & kPinnedRemoved) return false;
+    } while (!r.state.compare_exchange_weak(s, s + 1, std::memory_order_acq_rel));
     return true;
 }
+
+void pinned_release(PinnedRec& r) { r.state.fetch_sub(1, std::memory_order_acq_rel); }
 
 int device_cus() {
     static std::mutex mu;
@@ -156,6 +171,7 @@ struct pipck_ctx {
     uint32_t* d_pseudo = nullptr;
     void* d_flows = nullptr;
     uint32_t flows_cap = 0;
+    int zero_copy = 2;  // pipck_host_sum path (pipck_ctx_zero_copy)
     std::mutex mu;
 };
 
@@ -217,6 +233,7 @@ int pipck_ctx_create(int device, pipck_ctx** out) {
     }
     pipck_ctx* c = new pipck_ctx();
     c->device = device;
+    c->zero_copy = default_zero_copy();
     for (int i = 0; i < 2; i++) {
         PIPCK_HIP(hipStreamCreateWithFlags(&c->stream[i], hipStreamNonBlocking));
         PIPCK_HIP(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
@@ -274,7 +291,7 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
         off += ((size_t)segs[i].len + 15) & ~(size_t)15;
     }
     hipStream_t s = c->stream[0];
-    const int zc = g_zero_copy.load(std::memory_order_relaxed);
+    const int zc = c->zero_copy;
     if (zc == 1 || (zc == 2 && need <= kZeroCopyMax)) {
         // The kernel reads the pinned staging buffer over PCIe and writes the
         // result into pinned host memory: no copy commands around the launch.
@@ -309,7 +326,15 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
     return PIPCK_OK;
 }
 
-void pipck_host_zero_copy(int mode) { g_zero_copy.store(mode >= 0 && mode <= 2 ? mode : 2); }
+int pipck_ctx_zero_copy(pipck_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 2) {
+        set_error("pipck_ctx_zero_copy: null context or mode outside 0..2");
+        return PIPCK_EINVAL;
+    }
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->zero_copy = mode;
+    return PIPCK_OK;
+}
 
 int pipck_host_register(void* p, size_t bytes) {
     if (!p || !bytes) {
@@ -328,7 +353,15 @@ int pipck_host_register(void* p, size_t bytes) {
 }
 
 int pipck_host_unregister(void* p) {
-    pinned_remove(p);
+    const int rc = pinned_remove(p);
+    if (rc == PIPCK_EBUSY) {
+        set_error("pipck_host_unregister: a queued TX batch still reads this range in place");
+        return rc;
+    }
+    if (rc) {
+        set_error("pipck_host_unregister: not a range made by pipck_host_register");
+        return rc;
+    }
     PIPCK_HIP(hipHostUnregister(p));
     return PIPCK_OK;
 }
@@ -342,10 +375,19 @@ void* pipck_host_alloc(size_t bytes) {
     return p;
 }
 
-void pipck_host_free(void* p) {
-    if (!p) return;
-    pinned_remove(p);
-    (void)hipHostFree(p);
+int pipck_host_free(void* p) {
+    if (!p) return PIPCK_OK;
+    const int rc = pinned_remove(p);
+    if (rc == PIPCK_EBUSY) {
+        set_error("pipck_host_free: a queued TX batch still reads this buffer in place");
+        return rc;
+    }
+    if (rc) {
+        set_error("pipck_host_free: not a buffer from pipck_host_alloc");
+        return rc;
+    }
+    PIPCK_HIP(hipHostFree(p));
+    return PIPCK_OK;
 }
 
 int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride, uint32_t len, uint64_t n,

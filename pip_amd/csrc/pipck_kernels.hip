@@ -557,7 +557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
 }
 
 // ---------------------------------------------------------------------------
-// flat-stream kernel for tiny fixed strides (8-byte multiples, 8 .. 128 B)
+// flat-stream kernel for tiny fixed strides (8-byte multiples, 8 .. 64 B)
 // ---------------------------------------------------------------------------
 // cfg1's 20-byte IPv4 headers at a 24-byte stride.  A wave task of `run`
 // consecutive packets is streamed as coalesced 1 KiB rows through a ring of U

@@ -1,0 +1,40 @@
+/*
+ * pipck_testing.h -- INTERNAL tuning hook of libpipck.so, for the GPU tests and
+ * the measurement tools only (tests/, tools/).  Not part of the public ABI in
+ * include/pipck.h: it is process-global mutable state that changes kernel
+ * selection for every context and thread, so a product caller must never
+ * use it.  Every setting computes the same results (the GPU tests sweep them
+ * against the oracle); only speed changes.  pipck_tune(0, 0, 0, 0) restores
+ * the automatic choice.
+ */
+#ifndef PIPCK_TESTING_H
+#define PIPCK_TESTING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Launch-shape override for tuning; 0 = automatic everywhere (process-wide, internal).
+ * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
+ * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
+ * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9/13/17/25/33 =
+ * ring-pipelined 2/4/8/12/16/24/32); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
+ * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream
+ * fixed kernel, bit 3 = XCD-grouped task split, bit 4 = no packed-tile
+ * addressing in the ragged kernel, bit 5 = 4-wave ragged blocks (default 1),
+ * bit 6 = never the small-packet kernel (packets <= 64 B incl. chunk offset),
+ * bit 7 = never the short-stride flat kernel (16-B-multiple strides < 1 KiB),
+ * bits 8..15 = 1 KiB rows per flat-kernel wave task (default 64), bit 16 = no
+ * lane-per-segment path for ragged tiles of tiny segments, bit 17 = never the
+ * tiny-stride flat kernel (8-B-multiple strides <= 64 B with pseudo-headers or
+ * RX verify; loads_per_lane 4/8/16 = its ring, bits 8..15 its rows per wave
+ * task, default 4 and 12), bit 18 = that kernel without pseudo-headers too, bits 24..27 =
+ * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2). */
+void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIPCK_TESTING_H */

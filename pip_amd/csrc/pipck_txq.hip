@@ -99,12 +99,18 @@ struct TxBatch {
     std::vector<uint8_t*> inet_field;
     std::vector<pipck_desc> ip_hdrs;
     std::vector<uint8_t*> ip_field;
+    std::vector<PinnedRef> held;  // pinned ranges this batch reads in place (one hold each, released at complete)
     PinnedBuf meta;     // staging for descriptors/records and results
     DevBuf d_all;       // device copy of bytes + meta
     DevBuf d_work;      // pseudo bases, scratch, results
     size_t o_res = 0;   // offset of the results in `meta` (valid while in flight)
     uint64_t pending() const { return inet_field.size() + ip_field.size(); }
+    void drop_holds() {
+        for (PinnedRef& r : held) pinned_release(*r);
+        held.clear();
+    }
     void clear() {
+        drop_holds();
         bytes.size = 0;
         inet_segs.clear();
         has_zc = false;
@@ -115,6 +121,7 @@ struct TxBatch {
         ip_field.clear();
     }
     void release() {
+        drop_holds();
         bytes.release();
         meta.release();
         d_all.release();
@@ -132,9 +139,6 @@ struct pipck_txq {
     hipEvent_t done = nullptr;  // recorded after the in-flight batch's D2H copy
     int device = 0;
     TxBatch batch[2];
-    PinnedRange pin_cache[4];  // pinned ranges of recent zero-copy segments (headers and payloads
-    unsigned pin_next = 0;     // usually come from a few buffers): most checks skip the registry
-    uint64_t pin_gen = 0;      // registry generation the cache was filled under
     bool auto_zc = false;      // plain adds read pinned segments in place (pipck_txq_auto_zero_copy)
     int cur = 0;         // batch receiving adds
     bool inflight = false;  // batch[cur ^ 1] has been submitted and not completed
@@ -153,21 +157,23 @@ int append_bytes(TxBatch* b, const void* src, uint32_t len, uint64_t* off) {
     return PIPCK_OK;
 }
 
-// Is [p, p+len) inside a pinned range (pipck_host_alloc / pipck_host_register)?
-// The queue's 4-entry cache answers most checks; it is dropped whenever a range
-// has been removed since it was filled.
-bool seg_pinned(pipck_txq* q, const void* p, uint32_t len) {
-    const uint64_t gen = pinned_generation();
-    if (gen != q->pin_gen) {
-        for (PinnedRange& r : q->pin_cache) r = PinnedRange{};
-        q->pin_gen = gen;
-    }
+// Can [p, p+len) be read in place by batch b?  Only inside a pinned range
+// (pipck_host_alloc / pipck_host_register), and the batch then holds that
+// range until it completes, so the range cannot be freed or unregistered while
+// the GPU may still read it.  Segments of one batch usually come from a few
+// buffers (a header ring, a payload ring): the batch's held ranges answer most
+// checks without the registry.
+bool hold_pinned(TxBatch* b, const void* p, uint32_t len) {
     const uintptr_t a = (uintptr_t)p;
-    for (const PinnedRange& r : q->pin_cache)
-        if (a >= r.lo && a + len <= r.hi) return true;
-    PinnedRange r;
-    if (!pinned_lookup(p, len, &r)) return false;
-    q->pin_cache[q->pin_next++ % 4] = r;
+    // the most recently held ranges only, so a batch of many small buffers stays O(1)
+    // per segment (a range found in the registry again is simply held twice)
+    for (size_t i = b->held.size(), k = 0; i-- > 0 && k < 4; k++) {
+        const PinnedRec& r = *b->held[i];
+        if (a >= r.lo && a + len <= r.hi) return true;  // held: cannot have been removed
+    }
+    PinnedRef r = pinned_lookup(p, len);
+    if (!r || !pinned_acquire(*r)) return false;  // unpinned, or being released right now
+    b->held.push_back(std::move(r));
     return true;
 }
 
@@ -178,24 +184,25 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
         set_error("pipck_txq_add: null argument");
         return PIPCK_EINVAL;
     }
-    uint32_t in_place = 0;  // bit i: segment i is read in place (nseg <= 32 when any is)
     for (uint32_t i = 0; i < nseg; i++) {
         if (segs[i].len > PIPCK_MAX_SEG_LEN || (segs[i].len && !segs[i].ptr)) {
             set_error("pipck_txq_add: segment null or longer than 65535 bytes");
             return PIPCK_ERANGE;
         }
-        if (zc && segs[i].len && !seg_pinned(q, segs[i].ptr, segs[i].len)) {
-            // the GPU will read it in place: it must be pinned
+    }
+    TxBatch* b = &q->batch[q->cur];
+    const size_t seg0 = b->inet_segs.size(), bytes0 = b->bytes.size;
+    for (uint32_t i = 0; i < nseg; i++) {
+        const bool in_place = (zc || q->auto_zc) && segs[i].len && hold_pinned(b, segs[i].ptr, segs[i].len);
+        if (zc && segs[i].len && !in_place) {
+            // the GPU would read it in place: it must be pinned; drop this packet's segments
+            b->inet_segs.resize(seg0);
+            b->bytes.size = bytes0;
             set_error("pipck_txq_add_zc: segment outside every range from pipck_host_alloc / "
                       "pipck_host_register");
             return PIPCK_EINVAL;
         }
-        if (!zc && q->auto_zc && i < 32 && segs[i].len && seg_pinned(q, segs[i].ptr, segs[i].len))
-            in_place |= 1u << i;
-    }
-    TxBatch* b = &q->batch[q->cur];
-    for (uint32_t i = 0; i < nseg; i++) {
-        if (zc || (i < 32 && (in_place >> i & 1u))) {
+        if (in_place) {
             // read in place at flush time (pinned host memory, device-accessible at the same address)
             b->inet_segs.push_back(pipck_desc{(uint64_t)(uintptr_t)segs[i].ptr, segs[i].len, 1u});
             b->has_zc = true;
@@ -203,7 +210,11 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
         }
         uint64_t off = 0;
         int rc = append_bytes(b, segs[i].ptr, segs[i].len, &off);
-        if (rc) return rc;
+        if (rc) {
+            b->inet_segs.resize(seg0);
+            b->bytes.size = bytes0;
+            return rc;
+        }
         b->inet_segs.push_back(pipck_desc{off, segs[i].len, 0});
     }
     b->inet_begin.push_back(b->inet_segs.size());
@@ -334,8 +345,6 @@ int pipck_txq_create(pipck_ctx* ctx, pipck_txq** out) {
     pipck_txq* q = new pipck_txq();
     q->ctx = ctx;
     q->device = dev;
-    q->pin_gen = pinned_generation();
-    if (const char* e = getenv("PIPCK_TXQ_AUTO_ZERO_COPY")) q->auto_zc = atoi(e) != 0;
     if (hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&q->done, hipEventDisableTiming) != hipSuccess) {
         set_error("pipck_txq_create: stream/event creation failed");

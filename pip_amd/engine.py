@@ -190,7 +190,8 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          packed_tiles: bool = True, wide_blocks: bool = False,
          small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True,
          flat_tiny: bool = True, force_flat_tiny: bool = False) -> None:
-    """Process-wide launch-shape override (0 = automatic); see pipck_tune in include/pipck.h."""
+    """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
+    (pip_amd/csrc/pipck_testing.h), not part of the public ABI."""
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
              | (0 if packed_tiles else 16) | (32 if wide_blocks else 0) | (0 if small else 64)
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)

@@ -32,6 +32,45 @@ def dist_env() -> DistEnv:
                    int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(world: int, argv: list[str], port: int | None = None) -> int:
+    """Run ``argv`` as ranks 0..world-1 of a one-node job (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT in each child's environment),
+    the way ``torch.distributed.run --nnodes=1`` would.  The parent only waits:
+    it never touches the GPU (the children each pick theirs by LOCAL_RANK).
+    Returns 0, or the first failing rank's exit status (128 + signal for a
+    signal) after terminating the ranks still running."""
+    import subprocess
+    import time
+
+    port = port or free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(argv, env=env))
+    rc, running = 0, set(range(world))
+    while running:
+        for r in sorted(running):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            running.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in running:
+                    procs[q].terminate()
+        time.sleep(0.02)
+    return rc
+
+
 def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous, balanced packet-id range [first, first+count) of one rank."""
     if not 0 <= rank < world:
@@ -57,6 +96,29 @@ def shard_by_bytes(prefix_bytes: list[int] | tuple[int, ...], world: int, rank: 
 
     a, b = cut(rank), cut(rank + 1)
     return a, b - a
+
+
+def byte_cuts(prefix_bytes, world: int) -> list[int]:
+    """``shard_by_bytes`` for every rank at once over a large sorted prefix array
+    (numpy array or torch tensor, len == n_packets + 1): the N+1 packet indices
+    where the rank ranges begin/end.  ``searchsorted(side="left")`` is bisect_left."""
+    n = len(prefix_bytes) - 1
+    total = int(prefix_bytes[-1])
+    cuts = [0]
+    for r in range(1, world):
+        target = total * r // world
+        if hasattr(prefix_bytes, "cpu"):  # torch tensor (device-resident prefix)
+            import torch
+
+            at = int(torch.searchsorted(prefix_bytes, torch.tensor([target], dtype=prefix_bytes.dtype,
+                                                                    device=prefix_bytes.device)).item())
+        else:
+            import numpy as np
+
+            at = int(np.searchsorted(prefix_bytes, target, side="left"))
+        cuts.append(min(n, at))
+    cuts.append(n)
+    return cuts
 
 
 def init_control_plane(env: DistEnv) -> None:
@@ -97,6 +159,19 @@ def sum_over_ranks(env: DistEnv, value: float) -> float:
     t = torch.tensor([value], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def gather_over_ranks(env: DistEnv, values: list[float]) -> list[list[float]]:
+    """Every rank's ``values`` (same length on all ranks), indexed by rank."""
+    if not env.distributed:
+        return [list(values)]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(values, dtype=torch.float64)
+    out = [torch.empty_like(t) for _ in range(env.world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
 
 
 def shutdown(env: DistEnv) -> None:

@@ -18,6 +18,14 @@ def cfg_seed(cfg: int) -> int:
     return 0x9E3779B97F4A7C15 ^ cfg
 
 
+def count_text(n: int) -> str:
+    """8388608 -> '8M', 1000 -> '1000' (binary multiples, as BASELINE.json counts packets)."""
+    for shift, suffix in ((30, "G"), (20, "M"), (10, "K")):
+        if n >= 1 << shift and n % (1 << shift) == 0:
+            return f"{n >> shift}{suffix}"
+    return f"{n:,}"
+
+
 @dataclass(frozen=True)
 class Workload:
     name: str
@@ -28,7 +36,7 @@ class Workload:
     proto: int
     n_packets: int      # the BASELINE.json batch (cfg5: the whole 8-GPU job)
     stride: int = 0     # arena slot per packet (fixed configs)
-    description: str = ""
+    shape: str = ""     # packet shape, without the count
 
     @property
     def seed(self) -> int:
@@ -38,17 +46,28 @@ class Workload:
     def ragged(self) -> bool:
         return self.length is None
 
+    @property
+    def description(self) -> str:
+        return self.describe(self.n_packets)
 
-CFG1 = Workload("cfg1_ipv4_header", 1, 20, HDR_IPV4, 0, 0, 1 << 20, 24,
-                "IPv4 20-byte header checksum (pip_ip_checksum), 1M headers")
+    def describe(self, n_packets: int, n_gpus: int = 1) -> str:
+        """The workload as run: the packet count is the one actually checksummed."""
+        where = f" over {n_gpus} GPUs" if n_gpus > 1 else ""
+        return f"{self.shape}, {count_text(n_packets)} packets{where}"
+
+
+# cfg1 is laid out packed (stride 20 = the header): every fetched byte is a
+# header byte, so the launch's HBM traffic is the algorithmic 22 B per header.
+CFG1 = Workload("cfg1_ipv4_header", 1, 20, HDR_IPV4, 0, 0, 1 << 20, 20,
+                "IPv4 20-byte header checksum (pip_ip_checksum), packed 20-B stride")
 CFG2 = Workload("cfg2_tcp4_mtu1500", 2, 1480, HDR_TCP, 4, 6, 4 << 20, 1488,
-                "TCP/IPv4, 20-B header + 1460-B payload, 4M packets")
+                "TCP/IPv4, 20-B header + 1460-B payload")
 CFG3 = Workload("cfg3_udp6_mtu9000", 3, 8960, HDR_UDP, 6, 17, 1 << 20, 8960,
-                "UDP/IPv6, 8-B header + 8952-B payload, 1M packets")
+                "UDP/IPv6, 8-B header + 8952-B payload")
 CFG4 = Workload("cfg4_tcp4_zipf", 4, None, HDR_TCP, 4, 6, 8 << 20, 0,
-                "TCP/IPv4, L4 length 64-9000 B Zipf(1.0), 8M packets (ragged)")
+                "TCP/IPv4, L4 length 64-9000 B Zipf(1.0), ragged")
 CFG5 = Workload("cfg5_tcp4_mtu9000", 5, 8980, HDR_TCP, 4, 6, 64 << 20, 8992,
-                "TCP/IPv4 MTU 9000, 20-B header + 8960-B payload, 64M packets over 8 GPUs")
+                "TCP/IPv4 MTU 9000, 20-B header + 8960-B payload")
 
 ALL = {w.name: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5)}
 BY_CFG = {w.cfg: w for w in (CFG1, CFG2, CFG3, CFG4, CFG5)}

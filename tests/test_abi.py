@@ -42,6 +42,29 @@ def test_libpipck_exports_every_declared_function():
     assert sorted(_lib.SIGNATURES) == declared
 
 
+def test_internal_tuning_hook_is_outside_the_public_header():
+    internal = header_functions(ROOT / "pip_amd" / "csrc" / "pipck_testing.h")
+    assert internal == sorted(_lib.INTERNAL_SIGNATURES) == ["pipck_tune"]
+    assert "pipck_tune" in dynsyms(_lib.LIBPIPCK)  # still exported, for tests/ and tools/
+
+
+def test_public_header_has_no_process_global_knobs():
+    """Every mode switch in include/*.h is per context or per queue: a
+    declaration whose name speaks of tuning or zero-copy must take a
+    pipck_ctx* / pipck_txq* first; nothing reads a knob from the environment
+    except a new context's initial per-packet mode."""
+    for h in ("pipck.h", "pip_checksum_amd.h"):
+        text = re.sub(r"/\*.*?\*/|//[^\n]*", "", (ROOT / "include" / h).read_text(), flags=re.S)
+        for name, params in re.findall(r"\b(pip\w*(?:tune|zero_copy|capture)\w*)\s*\(([^)]*)\)", text):
+            if h == "pipck.h":
+                assert re.match(r"\s*(const\s+)?pipck_(ctx|txq)\s*\*", params), (name, params)
+            else:  # the drop-in's switches are per calling thread (thread_local queue)
+                assert name.startswith("pip_checksum_amd_"), name
+        assert "pipck_tune" not in text and "pipck_host_zero_copy" not in text
+    shim = (ROOT / "pip_amd" / "csrc" / "pip_checksum_shim.cpp").read_text()
+    assert "getenv" not in shim and "PIPCK_TXQ_AUTO_ZERO_COPY" not in (ROOT / "pip_amd" / "csrc" / "pipck_txq.hip").read_text()
+
+
 def test_libpipck_loads_and_reports_version():
     lib = _lib.load()
     assert lib.pipck_version() >> 16 == 1

@@ -26,9 +26,18 @@ def test_golden_replay_is_self_consistent():
 
 
 @pytest.mark.gpu
-def test_pip_stack_on_amd_checksum_is_byte_identical():
+@pytest.mark.parametrize("capture", [False, True])
+def test_pip_stack_on_amd_checksum_is_byte_identical(capture):
+    """capture: the same replay with the drop-in's capture mode on -- pip's
+    unchanged call sites queue their checksums and one flush per stack action
+    fills them before the packets are emitted."""
+    import os
+
     assert REPLAY_AMD.exists(), "build with `make -C oracle ref ref-amd` where /root/reference exists"
-    r = subprocess.run([str(REPLAY_AMD)], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ)
+    if capture:
+        env["PIPCK_REPLAY_CAPTURE"] = "1"
+    r = subprocess.run([str(REPLAY_AMD)], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     want = GOLDEN.read_text().strip().splitlines()
     got = r.stdout.strip().splitlines()
@@ -38,8 +47,12 @@ def test_pip_stack_on_amd_checksum_is_byte_identical():
     # the deferred (batched) API on real pip_buf chains, flushed in one GPU batch
     # and pipelined: submitted every 5 packets while the next are queued, then completed
     lines = [ln for ln in r.stderr.splitlines() if ln.startswith("DEFERRED")]
-    assert [ln.split()[2] for ln in lines] == ["flush", "pipelined"], r.stderr[-2000:]
+    # and zero-copy from pinned memory with every chain reference dropped before the flush
+    assert [ln.split()[2] for ln in lines] == ["flush", "pipelined", "zero_copy"], r.stderr[-2000:]
     for line in lines:
         f = line.split()
         assert f[f.index("bad") + 1] == "0" and f[f.index("pending_after") + 1] == "0", line
-        assert int(f[f.index("checked") + 1]) >= 40
+        assert int(f[f.index("checked") + 1]) >= 25
+    zc = lines[-1].split()
+    assert zc[zc.index("free_while_queued") + 1] == "6"  # PIPCK_EBUSY
+    assert zc[zc.index("free_after") + 1] == "0"

@@ -70,9 +70,9 @@ class PcAdapter:
 def staged_per_packet():
     """The per-packet path with staged copies (the default auto mode zero-copies small calls)."""
     lib = _lib.load()
-    lib.pipck_host_zero_copy(0)
+    checksum.set_zero_copy(0)
     yield
-    lib.pipck_host_zero_copy(2)
+    checksum.set_zero_copy(2)
 
 
 def test_every_known_answer_on_gpu(kat, staged_per_packet):
@@ -88,12 +88,12 @@ def test_every_known_answer_on_gpu_zero_copy(kat):
     """The same known answers through the zero-copy per-packet path (the kernel
     reads pinned host staging and writes the result to host memory)."""
     lib = _lib.load()
-    lib.pipck_host_zero_copy(1)
+    checksum.set_zero_copy(1)
     try:
         bad = [c["fn"] for c in kat if run_case(PcAdapter, c) != c["expect"]]
         assert not bad, bad[:5]
     finally:
-        lib.pipck_host_zero_copy(2)
+        checksum.set_zero_copy(2)
 
 
 def test_per_packet_api_is_thread_safe(kat):
@@ -930,27 +930,30 @@ def test_txq_zero_copy_segments(oracle, register, in_place, monkeypatch):
             lib.pipck_host_free(C.c_void_p(base))
 
 
-@pytest.mark.parametrize("env", [False, True])
-def test_txq_auto_zero_copy(oracle, env, monkeypatch):
-    """pipck_txq_auto_zero_copy (or PIPCK_TXQ_AUTO_ZERO_COPY=1 at creation):
-    plain add4/add6 read pinned segments in place and copy the rest.  Shown by
-    rewriting every source buffer after add and before flush: a pinned
-    segment's checksum follows the new bytes, a copied one keeps the add-time
-    bytes.  Then the pinned range is freed: the queue's range cache must drop
-    it, so a zero-copy add of the same address is refused (never read in place)."""
-    if env:
-        monkeypatch.setenv("PIPCK_TXQ_AUTO_ZERO_COPY", "1")
+@pytest.mark.parametrize("mode", ["api", "env_only"])
+def test_txq_auto_zero_copy(oracle, mode, monkeypatch):
+    """pipck_txq_auto_zero_copy: plain add4/add6 read pinned segments in place
+    and copy the rest.  Shown by rewriting every source buffer after add and
+    before flush: a pinned segment's checksum follows the new bytes, a copied
+    one keeps the add-time bytes.  The mode is an explicit per-queue opt-in:
+    PIPCK_TXQ_AUTO_ZERO_COPY in the environment alone changes nothing (every
+    segment keeps its add-time bytes).  Chains of more than 32 segments are read
+    in place segment by segment too.  A pinned range with queued in-place
+    segments cannot be freed (PIPCK_EBUSY) until their batch completes; once
+    freed, a zero-copy add of it is refused (never read in place)."""
+    monkeypatch.setenv("PIPCK_TXQ_AUTO_ZERO_COPY", "1")
+    auto = mode == "api"
     lib = _lib.load()
     ctx, q = C.c_void_p(), C.c_void_p()
     _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
     _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
-    if not env:
+    if auto:
         _lib.check("auto_zero_copy", lib.pipck_txq_auto_zero_copy(q, 1))
     size = 1 << 20
     base = lib.pipck_host_alloc(size)
     assert base
     pool = np.ctypeslib.as_array((C.c_uint8 * size).from_address(base))
-    rng = np.random.default_rng(77 + env)
+    rng = np.random.default_rng(77 + auto)
     freed = False
     try:
         n_pk = 300
@@ -958,20 +961,21 @@ def test_txq_auto_zero_copy(oracle, env, monkeypatch):
         keep, finals, pos = [], [], 0
         for i in range(n_pk):
             field = C.c_void_p(C.addressof(fields) + 2 * i)
-            nseg = int(rng.integers(1, 4))
+            nseg = 40 if i == 7 else int(rng.integers(1, 4))  # one chain longer than 32 segments
             arr = (_lib.HSeg * nseg)()
             segs_final = []
             for j in range(nseg):
                 ln = int(rng.choice([0, 20, int(rng.integers(1, 1500))]))
                 old = rng.integers(0, 256, ln, dtype=np.uint8)
                 new = rng.integers(0, 256, ln, dtype=np.uint8)
-                if rng.integers(0, 2):  # pinned: read at flush -> the rewritten bytes count
+                if rng.integers(0, 2) or (i == 7 and j >= 32):  # pinned
                     pos += int(rng.integers(0, 16))
                     pool[pos:pos + ln] = old
                     arr[j].ptr = C.c_void_p(base + pos)
                     keep.append(("pinned", pos, new))
                     pos += ln
-                    segs_final.append(new.tobytes())
+                    # read at flush in auto mode -> the rewritten bytes count
+                    segs_final.append(new.tobytes() if auto else old.tobytes())
                 else:  # ordinary memory: copied at add -> the add-time bytes count
                     b = C.create_string_buffer(old.tobytes(), max(ln, 1))
                     arr[j].ptr = C.cast(b, C.c_void_p)
@@ -993,16 +997,22 @@ def test_txq_auto_zero_copy(oracle, env, monkeypatch):
                 pool[where:where + len(new)] = new
             elif len(new):
                 C.memmove(where, new.tobytes(), len(new))
+        if auto:  # queued in-place segments hold the range
+            assert lib.pipck_host_free(C.c_void_p(base)) == _lib.PIPCK_EBUSY
+            assert b"in place" in lib.pipck_last_error()
         _lib.check("flush", lib.pipck_txq_flush(q))
         got = np.frombuffer(bytes(fields), dtype=">u2")
         assert np.array_equal(got, np.array(finals, dtype=np.uint16)), np.nonzero(got != finals)[0][:5]
-        # a freed range leaves the cache: zero-copy adds of it are refused
+        # submitted but not completed: still held
         seg = (_lib.HSeg * 1)()
         seg[0].ptr, seg[0].len = C.c_void_p(base + 64), 32
         fld = (C.c_uint8 * 2)()
         _lib.check("add4_zc", lib.pipck_txq_add4_zc(q, seg, 1, 6, 1, 2, C.cast(fld, C.c_void_p)))
-        _lib.check("flush", lib.pipck_txq_flush(q))
-        lib.pipck_host_free(C.c_void_p(base))
+        _lib.check("submit", lib.pipck_txq_submit(q))
+        assert lib.pipck_host_free(C.c_void_p(base)) == _lib.PIPCK_EBUSY
+        _lib.check("complete", lib.pipck_txq_complete(q))
+        # completed: the range can go, and a freed range is never read in place again
+        _lib.check("pipck_host_free", lib.pipck_host_free(C.c_void_p(base)))
         freed = True
         assert lib.pipck_txq_add4_zc(q, seg, 1, 6, 1, 2, C.cast(fld, C.c_void_p)) == _lib.PIPCK_EINVAL
         assert lib.pipck_txq_pending(q) == 0

@@ -78,6 +78,83 @@ def test_two_ranks_equal_one(oracle):
     assert np.array_equal(one[:2000], oracle.batch_fixed(host, w.stride, w.length, 2000, 4, 6, w.seed, N_FLOWS, 0))
 
 
+def _ragged_rank(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch
+
+    from pip_amd import engine, shard
+    from pip_amd.workloads import CFG4, N_FLOWS
+
+    env = shard.dist_env()
+    shard.init_control_plane(env)
+    torch.cuda.set_device(env.local_rank % torch.cuda.device_count())
+    w = CFG4
+    lens_all = torch.empty(n_total, dtype=torch.int32, device="cuda")
+    engine.call("pipck_gen_zipf_lengths", engine._ptr(lens_all), n_total, 0, w.seed, engine.current_stream())
+    prefix = torch.zeros(n_total + 1, dtype=torch.int64, device="cuda")
+    torch.cumsum(lens_all.to(torch.int64), 0, out=prefix[1:])
+    cuts = shard.byte_cuts(prefix, world)
+    first, count = cuts[rank], cuts[rank + 1] - cuts[rank]
+    arena, desc, lens = engine.gen_ragged(count, first, w.seed, w.hdr, N_FLOWS,
+                                          lengths=lens_all[first:first + count].clone())
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    out = engine.checksum_ragged(arena, desc, pseudo)
+    q.put((rank, int(lens.to(torch.int64).sum().item()), out.cpu().numpy().view(np.uint16).tobytes()))
+    shard.barrier(env)
+    shard.shutdown(env)
+
+
+def test_two_ranks_ragged_equal_bytes(oracle):
+    """cfg4 split at equal L4 bytes (shard.byte_cuts): the two shards' results
+    concatenate to the one-rank answer, and the byte split is balanced."""
+    import torch
+    import torch.multiprocessing as mp
+
+    from pip_amd import engine
+    from pip_amd.workloads import CFG4, N_FLOWS
+
+    n_total = 60_007
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_ragged_rank, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    b0, b1 = res[0][1], res[1][1]
+    assert abs(b0 - b1) <= 2 * 9000, (b0, b1)  # cut at a packet boundary: within one packet of half
+    got = np.frombuffer(b"".join(r[2] for r in res), dtype=np.uint16)
+    w = CFG4
+    arena, desc, _ = engine.gen_ragged(n_total, 0, w.seed, w.hdr, N_FLOWS)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    one = engine.checksum_ragged(arena, desc, pseudo).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, one)
+    h_arena, offs, lens = oracle.gen_ragged_batch(w.seed, 0, 3000, w.hdr)
+    assert np.array_equal(one[:3000], oracle.batch_ragged(h_arena, offs, lens, 4, 6, w.seed, N_FLOWS, 0))
+
+
+def test_bench_self_launch_cfg5_two_ranks():
+    """`python bench.py --gpus 2` with no torchrun: bench.py starts both ranks
+    itself (sharing the box's one GPU), each with a full cfg5 shard of 8M
+    8,980-byte packets (2 x 75 GB of HBM), and rank 0 prints one JSON line."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["config"]["global_packets"] == 2 * (8 << 20) and d["config"]["packets_per_gpu"] == 8 << 20
+    assert d["config"]["workload"].startswith("cfg5_tcp4_mtu9000") and "16M packets over 2 GPUs" in d["config"]["workload"]
+    assert len(d["per_rank_gib_per_s"]) == 2 and all(v > 0 for v in d["per_rank_gib_per_s"])
+    assert d["per_rank_packets"] == [8 << 20, 8 << 20]
+
+
 def test_bench_two_ranks_json_contract():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"), "--gpus", "2",
@@ -90,3 +167,16 @@ def test_bench_two_ranks_json_contract():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 3
     assert d["config"]["global_packets"] == 400000 and d["config"]["packets_per_gpu"] == 200000
     assert d["value"] > 0 and d["roofline"]["bound"] == "hbm" and d["cpu_baseline"] is None
+    assert len(d["per_rank_gib_per_s"]) == 2
+
+
+def test_bench_cfg4_two_ranks_byte_split():
+    """The ragged bench under two ranks splits the global Zipf batch at equal bytes."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "cfg4", "--steps", "2",
+           "--warmup", "1", "--packets-per-gpu", "300000", "--no-cpu"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["config"]["global_packets"] == 600000 and sum(d["per_rank_packets"]) == 600000
+    assert "equal bytes" in d["config"]["parallelism"]

@@ -95,3 +95,68 @@ def test_ragged_shards_regenerate_identically(oracle, world):
             a = whole[int(offs[first + i]):int(offs[first + i]) + int(lens[first + i])]
             b = part[int(poffs[i]):int(poffs[i]) + int(plens[i])]
             assert np.array_equal(a, b)
+
+
+def test_byte_cuts_match_shard_by_bytes():
+    import torch
+
+    rng = np.random.default_rng(11)
+    lens = rng.integers(64, 9001, 20000)
+    prefix = [0] + [int(x) for x in np.cumsum(lens)]
+    for world in (1, 2, 3, 4, 8):
+        want = [shard.shard_by_bytes(prefix, world, r) for r in range(world)]
+        for arr in (np.array(prefix, dtype=np.int64), torch.tensor(prefix, dtype=torch.int64)):
+            cuts = shard.byte_cuts(arr, world)
+            assert [(cuts[r], cuts[r + 1] - cuts[r]) for r in range(world)] == want
+
+
+_RANK_SCRIPT = """
+import os, sys
+sys.path.insert(0, {root!r})
+from pip_amd import shard
+env = shard.dist_env()
+shard.init_control_plane(env)
+got = shard.gather_over_ranks(env, [float(env.rank), float(env.local_rank), float(env.world)])
+shard.barrier(env)
+if env.rank == 0:
+    print("RANKS", got, flush=True)
+if env.rank == {fail_rank}:
+    sys.exit(7)
+shard.shutdown(env)
+"""
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_spawn_ranks_runs_a_gloo_job(tmp_path, capfd, fail_rank):
+    """bench.py's self-launch: N children with RANK/LOCAL_RANK/WORLD_SIZE and a
+    rendezvous on 127.0.0.1; a failing rank's status comes back."""
+    from pathlib import Path
+    import sys
+
+    root = str(Path(__file__).resolve().parents[1])
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT.format(root=root, fail_rank=fail_rank))
+    rc = shard.spawn_ranks(3, [sys.executable, str(script)])
+    out = capfd.readouterr().out
+    assert "RANKS [[0.0, 0.0, 3.0], [1.0, 1.0, 3.0], [2.0, 2.0, 3.0]]" in out
+    assert rc == (7 if fail_rank == 1 else 0)
+
+
+def test_bench_refuses_world_size_mismatch(monkeypatch):
+    """Under torch.distributed.run, WORLD_SIZE must equal --gpus (checked before
+    anything touches the GPU)."""
+    import bench
+
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.main(["--gpus", "4"]) == 2
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.main(["--gpus", "2"]) == 2
+
+
+def test_workload_text_states_the_real_count():
+    from pip_amd.workloads import CFG1, CFG5
+
+    assert CFG5.describe(64 << 20, 8).endswith("64M packets over 8 GPUs")
+    assert CFG1.describe(256 << 20) .endswith("256M packets")
+    assert CFG1.describe(1000).endswith("1,000 packets")
+    assert CFG1.stride == 20 == CFG1.length  # packed headers: no slot padding

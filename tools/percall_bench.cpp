@@ -7,8 +7,10 @@
 // (and a 65,535-B one) (pip_inet_checksum): median and p99 microseconds per call on one thread,
 // for the staged path (H2D copy, kernel, D2H copy) and the zero-copy path
 // (the kernel reads the pinned staging buffer and writes the result to
-// pinned host memory directly; pipck_host_zero_copy(1)).  Results of both
-// paths are checked equal.  One JSON line per (size, path).
+// pinned host memory directly) -- both through pipck_host_sum on a context of
+// this tool's own (pipck_ctx_zero_copy 0 / 1), the call the drop-in makes --
+// and the drop-in itself in its default mode.  Results of all paths are
+// checked equal.  One JSON line per (size, path).
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -25,29 +27,47 @@ int main(int argc, char** argv) {
     struct in_addr s, d;
     s.s_addr = 0x0100000Au;
     d.s_addr = 0x0200000Au;
+    pipck_ctx* ctx = nullptr;
+    if (pipck_ctx_create(-1, &ctx)) {
+        fprintf(stderr, "percall_bench: %s\n", pipck_last_error());
+        return 1;
+    }
+    static const char* kPath[] = {"staged", "zero_copy", "drop_in"};
     for (uint32_t len : {20u, 1480u, 8980u, 65535u}) {
         uint32_t ref = 0;
-        for (int zc = 0; zc < 2; zc++) {
-            pipck_host_zero_copy(zc);
+        for (int path = 0; path < 3; path++) {
+            if (path < 2) pipck_ctx_zero_copy(ctx, path);
             std::vector<double> us;
             uint32_t r = 0;
             for (int i = 0; i < calls + 50; i++) {
                 auto t0 = std::chrono::steady_clock::now();
-                r = len == 20 ? pip_ip_checksum(buf.data(), len)
-                              : pip_inet_checksum(buf.data(), 6, s, d, (uint16_t)len);
+                if (path == 2) {
+                    r = len == 20 ? pip_ip_checksum(buf.data(), len)
+                                  : pip_inet_checksum(buf.data(), 6, s, d, (uint16_t)len);
+                } else {  // what the drop-in computes: pip's folded sum, then ~ (pip_checksum.cpp:35-61)
+                    const uint32_t pseudo = len == 20 ? 0u : 0x0A00u + 0x0001u + 0x0A00u + 0x0002u + 6u + len;  // 10.0.0.1 -> 10.0.0.2, TCP
+                    pipck_hseg seg{buf.data(), len};
+                    uint32_t sum = 0;
+                    if (pipck_host_sum(ctx, &seg, 1, pseudo, &sum)) {
+                        fprintf(stderr, "percall_bench: %s\n", pipck_last_error());
+                        return 1;
+                    }
+                    r = (uint16_t)~(uint16_t)sum;
+                }
                 auto t1 = std::chrono::steady_clock::now();
                 if (i >= 50) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
             }
-            if (zc == 0) ref = r;
+            if (path == 0) ref = r;
             if (r != ref) {
-                fprintf(stderr, "percall_bench: zero-copy result %u != staged %u at len %u\n", r, ref, len);
+                fprintf(stderr, "percall_bench: %s result %u != staged %u at len %u\n", kPath[path], r, ref, len);
                 return 1;
             }
             std::sort(us.begin(), us.end());
             printf("{\"tool\": \"percall_bench\", \"len\": %u, \"path\": \"%s\", \"median_us\": %.2f, \"p99_us\": %.2f}\n",
-                   len, zc ? "zero_copy" : "staged", us[us.size() / 2], us[us.size() * 99 / 100]);
+                   len, kPath[path], us[us.size() / 2], us[us.size() * 99 / 100]);
             fflush(stdout);
         }
     }
+    pipck_ctx_destroy(ctx);
     return 0;
 }
