@@ -46,6 +46,8 @@ from pip_amd.workloads import ALL, BY_CFG, N_FLOWS  # noqa: E402
 METRIC = "GiB/s payload checksummed (device-resident), MTU-9000 TCP batch; Mpkt/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PER_GPU_PACKETS = 8 << 20  # cfg5: 64M packets over 8 GPUs
+# the kernel each config's launch runs (a PMC traffic file applies to that kernel only)
+KERNEL_OF = {1: "k_small", 2: "k_flat<", 3: "k_flat<", 4: "k_packed", 5: "k_flat<"}
 
 
 def parse(argv=None):
@@ -123,11 +125,13 @@ def run_rank(args) -> int:
             del lens_all, prefix
         else:
             first, count, lens = 0, n_total, None
-        arena, desc, lens = engine.gen_ragged(count, first, w.seed, w.hdr, N_FLOWS, lengths=lens)
+        # the packed layout: packets back to back at 16-byte granularity, u16
+        # lengths + one u64 per 64 packets instead of 16-byte descriptors
+        arena, lens16, tile_chunk, lens = engine.gen_packed(count, first, w.seed, w.hdr, lengths=lens)
         l4_bytes = int(lens.to(torch.int64).sum().item())
 
         def step(out):
-            return engine.checksum_ragged(arena, desc, pseudo, out=out)
+            return engine.checksum_packed(arena, lens16, tile_chunk, count, pseudo, N_FLOWS, None, first, out=out)
     else:
         first, count = shard.shard_range(n_total, env.world, env.rank)
         arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
@@ -177,8 +181,9 @@ def run_rank(args) -> int:
     tpath = Path(args.traffic) if args.traffic != "auto" else ROOT / "profiles" / f"traffic_cfg{w.cfg}.json"
     if args.traffic and tpath.exists():
         t = json.loads(tpath.read_text())
-        # only valid for the launch it was measured on: same kernel shape and per-launch byte count
-        if t.get("algorithmic_bytes_per_launch") == algo_bytes:
+        # only valid for the launch it was measured on: same kernel, layout and per-launch byte count
+        if (t.get("algorithmic_bytes_per_launch") == algo_bytes and t.get("arena_stride") == w.stride
+                and KERNEL_OF[w.cfg] in t.get("kernel", "")):
             traffic = t.get("hbm_bytes_per_launch")
 
     line = {

@@ -99,6 +99,29 @@ typedef struct pipck_desc {
 int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
                           const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_err, void* stream);
 
+/* Packed ragged batch: per-packet lengths, no per-packet descriptors.
+ * Packets lie back to back, each starting 16-byte aligned where the previous
+ * one's bytes end rounded up to 16: packet i is at d_arena + 16 * c_i, with c_i
+ * the sum of ceil(len_j / 16) over j < i (the layout of a TX staging arena and
+ * of the synthetic cfg4 batches).  d_lens[i] = packet i's length (u16, so in
+ * the batch domain by construction).  d_tile_chunk[t] = c_{64 t} for
+ * t = 0 .. ceil(n/64) -- one u64 per 64 packets (pipck_packed_index builds it;
+ * a producer that packs the arena knows it anyway) -- so the kernel reads 2 +
+ * 1/8 bytes of metadata per packet instead of a 16-byte pipck_desc.  Flow of
+ * packet i: d_flow_of ? d_flow_of[i] : (flow_origin + i) % n_flows; d_pseudo ==
+ * NULL = pip_ip_checksum semantics.  Results as pipck_checksum_ragged
+ * (pip_inet{,6}_checksum, pip_checksum.cpp:42-87).  d_arena 16-byte aligned. */
+int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
+                          uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                          uint64_t flow_origin, uint16_t* d_out, void* stream);
+/* RX verification of a packed batch (d_ok[i] = 1 iff packet i sums to 0xFFFF). */
+int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
+                        uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                        uint64_t flow_origin, uint8_t* d_ok, void* stream);
+/* Build d_tile_chunk (ceil(n/64) + 1 u64 entries; the last = the arena's 16-byte
+ * chunks) from the lengths, on the stream. */
+int pipck_packed_index(const uint16_t* d_lens, uint64_t n_packets, uint64_t* d_tile_chunk, void* stream);
+
 /* Chains (pip_buf lists, pip_checksum.cpp:90-148): packet p owns segments
  * [d_seg_begin[p], d_seg_begin[p+1]); its pseudo-header length term is the
  * u32 sum of its segment lengths (pip_buf::total_len).  Every segment is

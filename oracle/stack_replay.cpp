@@ -343,6 +343,10 @@ int main() {
     if (getenv("PIPCK_REPLAY_CAPTURE")) {
         pip_checksum_amd_capture(true);
         g_capture = true;
+        // warm the thread's TX queue (stream, pinned staging, kernels) so the first
+        // real flush does not stretch a session past pip's 1 s retransmit timer
+        pip_ip_checksum(z, 20);
+        pip_checksum_amd_flush();
     }
 #endif
     auto& nif = pip_netif::shared();

@@ -68,6 +68,18 @@ __device__ __forceinline__ uint64_t sum4(u32x4 v) {
     return (uint64_t)v.x + (uint64_t)v.y + (uint64_t)v.z + (uint64_t)v.w;
 }
 
+// lo16(w) + hi16(w) + acc in one v_dot2_u32_u16 against (1, 1): residue- and
+// zero-preserving like the folds above, and a u32 cannot overflow before
+// 2^32 / (2 * 0xFFFF) = 32768 dwords have been added.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot_fold(uint32_t w, uint32_t acc) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), u16x2{1, 1}, acc, false);
+}
+// A 16-byte chunk added into a u32 partial with four dot2 ops (<= 2^19 per chunk)
+__device__ __forceinline__ uint32_t dot4(const u32x4& v, uint32_t acc) {
+    return dot_fold(v.w, dot_fold(v.z, dot_fold(v.y, dot_fold(v.x, acc))));
+}
+
 // LE residue sum of a segment -> pip's big-endian folded segment sum in [0,0xFFFF]
 __device__ __forceinline__ uint32_t be_fold(uint32_t le_residue_sum, uintptr_t seg_addr) {
     uint32_t w = fold16(le_residue_sum);

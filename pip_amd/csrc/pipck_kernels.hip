@@ -579,10 +579,6 @@ constexpr uint32_t kForceFlatTiny = 1u << 18;  // bit 18: k_flat_tiny without ps
 constexpr uint32_t kFlatTinyMaxHalves = 8;  // strides up to 64 B
 constexpr uint32_t kFlatTinyMaxRun = 2048;  // packets per wave task
 
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t dot_fold(uint32_t w, uint32_t acc) {  // lo16(w) + hi16(w) + acc
-    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), u16x2{1, 1}, acc, false);
-}
 // Rows per LDS group for a stride of hpp 8-byte halves: the fewest whole rows
 // holding a whole number of packets, doubled until that is >= 64 packets.
 __host__ __device__ constexpr uint32_t tiny_group_rows(uint32_t hpp) {
@@ -776,27 +772,27 @@ __device__ __forceinline__ void ragged_issue(const RaggedTileLds& t, uint32_t c0
     for (int u = 0; u < U; u++) ragged_issue_row<NT>(t, c0 + u * 64, total, lane, v[u], sx[u], scur, packed, tbase);
 }
 
-// Add a run of whole rows of one segment (per-lane partials in racc) to the
+// Add a run of whole rows of one segment (per-lane u32 partials in racc) to the
 // segment's LDS partial: one wave sum, one LDS add.
-__device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint64_t& racc, uint32_t& rseg) {
+__device__ __forceinline__ void ragged_flush(RaggedTileLds& t, int lane, uint32_t& racc, uint32_t& rseg) {
     if (rseg == kNoSeg) return;  // wave-uniform
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(fold64(racc)), 63);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(racc), 63);
     if (lane == 0) atomicAdd(&t.acc[rseg], tot);
     racc = 0;
     rseg = kNoSeg;
 }
 
-// Reduce one row by segment.  A row lying wholly inside one segment (most rows
-// of multi-KiB packets) only adds into the per-lane run partial racc.  Any
-// other row takes a wave prefix scan: the lane holding a segment's last chunk
-// in the row adds (its prefix - the prefix just before the segment's first
-// chunk in the row) to the segment's LDS partial.  row < total (wave-uniform).
+// Reduce one row by segment (the lookup path: tiles that are not packed).  A
+// row lying wholly inside one segment only adds into the per-lane run partial
+// racc.  Any other row takes a wave prefix scan: the lane holding a segment's
+// last chunk in the row adds (its prefix - the prefix just before the
+// segment's first chunk in the row) to the segment's LDS partial.
+// row < total (wave-uniform).
 __device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
-                                                  const u32x4& v, uint32_t sx, uint64_t& racc, uint32_t& rseg,
-                                                  bool packed, uint32_t& scur) {
+                                                  const u32x4& v, uint32_t sx, uint32_t& racc, uint32_t& rseg) {
     const uint32_t c = row + lane;
     const bool active = c < total;
-    const uint32_t s = packed ? ragged_seg_of(t, c, scur) : sx;
+    const uint32_t s = sx;
     const uint32_t pre = t.pre[s];
     const uint32_t span = t.span[s];
     const int rel = (int)(c - pre);
@@ -805,7 +801,7 @@ __device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row
     u32x4 x = v;
     if (lo != 0) x = mask_chunk(x, lo, hi);  // a misaligned first chunk (rare)
     else if (hi < 16) x = mask_tail(x, hi);
-    const uint32_t val = active ? fold64(sum4(x)) : 0u;
+    const uint32_t val = active ? dot4(x, 0u) : 0u;
     const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
     const uint32_t end0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.pre[s0 + 1]);
     rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
@@ -841,23 +837,33 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     return v;
 }
 
-// Reduce one row of a packed tile.  Lane i of the wave holds segment i's
-// chunk range [pre_v, end_v) in registers, so the segment s0 of the row's
-// first chunk is a ballot popcount (pre is non-decreasing: the segments
-// starting at or before chunk c are a prefix), kept as scalars across rows.
-// A row strictly inside s0 (e0 > row + 64: no segment end, and packed
-// segments have no head bytes) needs no per-lane lookup or mask at all: its
-// chunks just add into the u64 run partial.  A mixed row finds every lane's
-// segment without a search: each segment starting inside the row marks its
-// first chunk's slot (LDS max, tagged by row so stale marks lose), and a wave
-// max-scan seeded with s0 carries the last start to every later lane.
+// Segment ends a mixed row walks in scalar code; beyond this many the row
+// finds its lanes' segments through LDS start marks instead.
+constexpr uint32_t kRowEndsLoop = 4;
+constexpr uint32_t kPackedMarksOnly = 1u << 19;  // pipck_tune flags bit 19: mixed rows always take the marks
+
+// Reduce one row of a packed tile (every segment starts 16-byte aligned where
+// the previous one's chunks end).  Lane i of the wave holds segment i's start
+// chunk pre_v and endt_v = end chunk | (len & 15) << 24.  The segment s0 of
+// the row's first chunk is a ballot popcount (starts are non-decreasing),
+// kept as scalars across rows.
+//  * Interior row (s0 ends past the row): all 64 chunks are whole chunks of
+//    s0 -- four dot2 ops into the lane's u32 run partial, nothing else.
+//  * Mixed row: the segments ending inside the row are s0 .. s0+k-1 (a
+//    ballot).  For k <= kRowEndsLoop a scalar loop reads each end E and tail
+//    length (v_readlane) and every lane derives its segment (count of ends
+//    <= its chunk), its head/tail flags and its tail mask with a few compares
+//    -- no LDS round trip; more ends than that (rows of tiny segments) use LDS
+//    start marks and a DPP max-scan.  Either way the row reduces by segment
+//    with one DPP prefix scan and fire-and-forget LDS adds (head/tail trick),
+//    and the run partial of the segment that ends here joins s0's tail lane.
 __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
-                                                         const u32x4& v, uint32_t pre_v, uint32_t end_v,
-                                                         uint32_t& s0, uint32_t& e0, uint64_t& racc,
-                                                         uint32_t& rseg) {
+                                                         const u32x4& v, uint32_t pre_v, uint32_t endt_v,
+                                                         uint32_t& s0, uint32_t& e0, uint32_t& racc, uint32_t& rseg,
+                                                         uint32_t kflags) {
     if (row >= e0) {  // wave-uniform: the row starts past segment s0
         s0 = (uint32_t)__popcll(__ballot(pre_v <= row)) - 1u;
-        e0 = (uint32_t)__builtin_amdgcn_readlane((int)end_v, (int)s0);
+        e0 = (uint32_t)__builtin_amdgcn_readlane((int)endt_v, (int)s0) & 0xFFFFFFu;
     }
     s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
     e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e0);
@@ -867,38 +873,62 @@ __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint3
             ragged_flush(t, lane, racc, rseg);
             rseg = s0;
         }
-        racc += sum4(v);
+        racc = dot4(v, racc);
         return;
     }
-    ragged_flush(t, lane, racc, rseg);
-    const uint32_t tag = ((row >> 6) + 1u) << 6;
-    if (pre_v > row && pre_v < row + 64) atomicMax(&t.mark[pre_v - row], tag | (uint32_t)lane);
-    wave_sync();
-    const uint32_t m = t.mark[lane];
-    const uint32_t s = wave_incl_max(lane == 0 ? s0 : (m >= tag ? (m & 63u) : 0u));
+    // the run (whole rows of one segment) ends here: its wave total R joins
+    // s0's tail contribution when it is s0's, else it is added on its own
+    uint32_t R = 0;
+    if (rseg != kNoSeg) {
+        R = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(racc), 63);
+        if (rseg != s0) {
+            if (lane == 0) atomicAdd(&t.acc[rseg], R);
+            R = 0;
+        }
+        racc = 0;
+        rseg = kNoSeg;
+    }
     const uint32_t c = row + lane;
     const bool active = c < total;
-    const int rel = (int)(c - t.pre[s]);
-    const int hi = (int)(t.span[s] >> 4) - 16 * rel;  // packed: no head bytes
+    const uint32_t end_v = endt_v & 0xFFFFFFu;
+    const uint32_t k = (uint32_t)__popcll(__ballot(end_v > row && end_v <= row + 64));  // ends s0 .. s0+k-1
+    uint32_t s;
+    bool head, tail;
     u32x4 x = v;
-    if (hi < 16) x = mask_tail(x, hi);
-    const uint32_t val = active ? fold64(sum4(x)) : 0u;
-    // segment sums by the head/tail prefix trick (see ragged_reduce_row)
-    const uint32_t inc = wave_incl_scan(val);
-    const bool tail = active && (lane == 63 || hi <= 16);
-    const bool head = active && rel == 0 && lane > 0;
-    if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
-}
-
-template <int U>
-__device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uint32_t total, int lane,
-                                              const u32x4 (&v)[U], const uint32_t (&sx)[U], uint64_t& racc,
-                                              uint32_t& rseg, bool packed, uint32_t& scur) {
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t row = c0 + u * 64;
-        if (row < total) ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, packed, scur);  // wave-uniform
+    if (k <= kRowEndsLoop && !(kflags & kPackedMarksOnly)) {
+        s = s0;
+        head = false;
+        tail = lane == 63;
+        for (uint32_t j = 0; j < k; j++) {  // scalar loop over the row's segment ends
+            const uint32_t et = (uint32_t)__builtin_amdgcn_readlane((int)endt_v, (int)(s0 + j));
+            const uint32_t E = et & 0xFFFFFFu, tl = et >> 24;
+            s += c >= E ? 1u : 0u;
+            head = head || c == E;
+            const bool last = c + 1 == E;
+            tail = tail || last;
+            if (tl && last) x = mask_tail(x, (int)tl);  // tl is wave-uniform: the mask is scalar
+        }
+    } else {
+        // each segment starting inside the row marks its first chunk's slot (LDS
+        // max, tagged by row so stale marks lose); a max-scan seeded with s0
+        // carries the last start to every later lane
+        const uint32_t tag = ((row >> 6) + 1u) << 6;
+        if (pre_v > row && pre_v < row + 64) atomicMax(&t.mark[pre_v - row], tag | (uint32_t)lane);
+        wave_sync();
+        const uint32_t m = t.mark[lane];
+        s = wave_incl_max(lane == 0 ? s0 : (m >= tag ? (m & 63u) : 0u));
+        const int rel = (int)(c - t.pre[s]);
+        const int hi = (int)(t.span[s] >> 4) - 16 * rel;  // packed: no head bytes
+        if (hi < 16) x = mask_tail(x, hi);
+        tail = lane == 63 || hi <= 16;
+        head = rel == 0;
     }
+    const uint32_t val = active ? dot4(x, 0u) : 0u;
+    const uint32_t inc = wave_incl_scan(val);
+    tail = tail && active;
+    head = head && active && lane > 0;
+    const uint32_t add = (tail ? inc + (s == s0 ? R : 0u) : 0u) - (head ? inc - val : 0u);
+    if (tail || head) atomicAdd(&t.acc[s], add);
 }
 
 // Stream a tile's chunks U rows at a time and reduce them by segment.
@@ -907,41 +937,82 @@ __device__ __forceinline__ void ragged_reduce(RaggedTileLds& t, uint32_t c0, uin
 // queue run dry while it reduces a batch) at no extra VGPRs.
 template <int U, bool PIPE, bool NT, bool PACKED>
 __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, int lane, uintptr_t tbase,
-                                              uint32_t pre_v, uint32_t end_v, uint64_t& racc, uint32_t& rseg) {
+                                              uint32_t pre_v, uint32_t endt_v, uint32_t& racc, uint32_t& rseg,
+                                              uint32_t kflags) {
     u32x4 v[U];
     uint32_t sx[U];
-    uint32_t scur = 0, rcur = 0;
+    uint32_t scur = 0;
     uint32_t s0 = 0, e0 = 0;  // packed: segment of the row's first chunk and its end (scalars)
     if (!total) return;
     ragged_issue<U, NT>(t, 0, total, lane, v, sx, scur, PACKED, tbase);
     for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
-        if (PIPE) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint32_t row = c0 + u * 64;
-                if (row < total) {  // wave-uniform
-                    if (PACKED)
-                        ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, end_v, s0, e0, racc, rseg);
-                    else
-                        ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg, false, rcur);
-                }
+        for (int u = 0; u < U; u++) {
+            const uint32_t row = c0 + u * 64;
+            if (row < total) {  // wave-uniform
+                if (PACKED)
+                    ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, endt_v, s0, e0, racc, rseg, kflags);
+                else
+                    ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg);
+            }
+            if (PIPE) {
                 // unconditional (clamped) reload: the VM count stays static, so each
                 // reduce waits for its own row only (vmcnt(U-1))
                 ragged_issue_row<NT>(t, row + 64 * U, total, lane, v[u], sx[u], scur, PACKED, tbase);
             }
-        } else {
-            if (PACKED) {
-#pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const uint32_t row = c0 + u * 64;
-                    if (row < total) ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, end_v, s0, e0, racc, rseg);
-                }
-            } else {
-                ragged_reduce<U>(t, c0, total, lane, v, sx, racc, rseg, false, rcur);
-            }
-            if (c0 + 64 * U < total) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
         }
+        if (!PIPE && c0 + 64 * U < total) ragged_issue<U, NT>(t, c0 + 64 * U, total, lane, v, sx, scur, PACKED, tbase);
     }
+}
+
+// The chunk stream of one tile of up to 64 segments (lane i = segment i, its
+// bytes at addr, nch chunks counting its head offset, head = addr & 15) ->
+// each lane's LE residue sum.  Tiles whose segments all fit kTinyChunks are
+// summed lane-per-segment; packed tiles stream 16 B x 64 rows from the first
+// segment's base; others map chunks to segments through the LDS prefix.
+template <int U, bool PIPE, bool NT>
+__device__ __forceinline__ uint32_t ragged_tile_sum(RaggedTileLds& t, int lane, uintptr_t addr, uint32_t head,
+                                                    uint32_t len, uint32_t nch, bool packed_hint, uint32_t kflags) {
+    if (__all(nch <= kTinyChunks) && !(kflags & kNoTinyTiles)) {
+        // Tiny-segment tile (IPv4 headers, bare TCP/UDP headers): every lane
+        // sums its own segment with its loads all in flight; no chunk stream.
+        const u32x4* b = reinterpret_cast<const u32x4*>(addr - head);
+        u32x4 v[kTinyChunks];
+#pragma unroll
+        for (uint32_t j = 0; j < kTinyChunks; j++)
+            v[j] = j < nch ? (NT ? load_stream(b + j) : load_plain(b + j)) : u32x4{0u, 0u, 0u, 0u};
+        uint32_t acc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kTinyChunks; j++) {
+            const int lo = j == 0 ? (int)head : 0;
+            const int hi = (int)(head + len) - 16 * (int)j;
+            u32x4 x = v[j];
+            if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+            acc = dot4(x, acc);
+        }
+        return acc;
+    }
+    const uint32_t incl = wave_incl_scan(nch);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    t.pre[lane] = incl - nch;
+    if (lane == 63) t.pre[64] = incl;
+    t.span[lane] = ((head + len) << 4) | head;
+    t.base[lane] = addr - head;
+    t.acc[lane] = 0;
+    t.mark[lane] = 0;
+    const bool packed = (kflags & kNoPackedTiles) == 0 && packed_hint;
+    const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
+    wave_sync();
+    uint32_t racc = 0;
+    uint32_t rseg = kNoSeg;
+    if (packed)
+        ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl | (len & 15u) << 24, racc, rseg,
+                                         kflags);
+    else  // fewer rows in flight: the lookup path needs a segment register per row
+        ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg, kflags);
+    ragged_flush(t, lane, racc, rseg);
+    wave_sync();
+    return t.acc[lane];
 }
 
 // One tile per wave, and by default one wave per block: tiles differ in size,
@@ -974,52 +1045,13 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         const uintptr_t addr = (uintptr_t)arena + d.offset;
         const uint32_t head = (uint32_t)(addr & 15);
         const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
-        uint32_t le_sum;
-        if (__all(nch <= kTinyChunks) && !(kflags & kNoTinyTiles)) {
-            // Tiny-segment tile (IPv4 headers, bare TCP/UDP headers): every lane
-            // sums its own segment with its loads all in flight; no chunk stream.
-            const u32x4* b = reinterpret_cast<const u32x4*>(addr - head);
-            u32x4 v[kTinyChunks];
-#pragma unroll
-            for (uint32_t j = 0; j < kTinyChunks; j++)
-                v[j] = j < nch ? (NT ? load_stream(b + j) : load_plain(b + j)) : u32x4{0u, 0u, 0u, 0u};
-            uint64_t acc = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < kTinyChunks; j++) {
-                const int lo = j == 0 ? (int)head : 0;
-                const int hi = (int)(head + len) - 16 * (int)j;
-                u32x4 x = v[j];
-                if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
-                acc += sum4(x);
-            }
-            le_sum = fold64(acc);
-        } else {
-            const uint32_t incl = wave_incl_scan(nch);
-            const uint32_t total = __shfl(incl, 63, 64);
-            t.pre[lane] = incl - nch;
-            if (lane == 63) t.pre[64] = incl;
-            t.span[lane] = ((head + len) << 4) | head;
-            t.base[lane] = addr - head;
-            t.acc[lane] = 0;
-            t.mark[lane] = 0;
-            // Packed tile: every segment starts 16-byte aligned right where the
-            // previous one's chunks end (the layout of pip's TX batches and of the
-            // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
-            const uint64_t next_off = (uint64_t)__shfl_down((long long)d.offset, 1, 64);
-            const bool link = lane == 63 || seg + 1 >= n || d.offset + 16ull * nch == next_off;
-            const bool packed = (kflags & kNoPackedTiles) == 0 && __all(head == 0 && link);
-            const uintptr_t tbase = (uintptr_t)first_lane_u64(addr);
-            wave_sync();
-            uint64_t racc = 0;
-            uint32_t rseg = kNoSeg;
-            if (packed)
-                ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
-            else  // fewer rows in flight: the lookup path needs a segment register per row
-                ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg);
-            ragged_flush(t, lane, racc, rseg);
-            wave_sync();
-            le_sum = t.acc[lane];
-        }
+        // Packed tile: every segment starts 16-byte aligned right where the
+        // previous one's chunks end (the layout of pip's TX batches and of the
+        // synthetic arenas), so chunk c of the tile is at base[0] + 16c.
+        const uint64_t next_off = (uint64_t)__shfl_down((long long)d.offset, 1, 64);
+        const bool link = lane == 63 || seg + 1 >= n || d.offset + 16ull * nch == next_off;
+        const bool packed = __all(head == 0 && link);
+        const uint32_t le_sum = ragged_tile_sum<U, PIPE, NT>(t, lane, addr, head, len, nch, packed, kflags);
         if (valid) {
             const uint32_t F = bad ? 0u : be_fold(le_sum, addr);
             if (FINAL) {
@@ -1035,6 +1067,81 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         }
         wave_sync();
     }
+}
+
+// ---------------------------------------------------------------------------
+// packed ragged batches: lengths only, no per-packet descriptors
+// ---------------------------------------------------------------------------
+// Packet i starts at arena + 16 * c_i, c_i = the chunks (lengths rounded up to
+// 16) of every earlier packet; tile_chunk[t] = c_{64t}.  The wave reads its 64
+// u16 lengths (128 B) and one u64, derives every offset with a wave prefix
+// scan of the chunk counts, and streams the tile as a packed tile of
+// k_ragged.  Metadata per packet: 2 B + 1/8 B instead of a 16-byte
+// descriptor.  One tile per wave, one wave per block.
+template <bool VERIFY, int U, bool NT>
+__global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
+                                               const uint64_t* __restrict__ tile_chunk, uint64_t n,
+                                               const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    __shared__ RaggedTileLds t;
+    const int lane = threadIdx.x & 63;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t seg = tile * 64 + lane;
+    const bool valid = seg < n;
+    const uint32_t len = valid ? lens[seg] : 0u;
+    uint32_t Pbase = 0;
+    if (pseudo && valid) {  // loaded now so the tile's end waits on nothing
+        const uint32_t f0 = (uint32_t)((flow_origin + tile * 64) % n_flows);  // one 64-bit modulo per tile
+        Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
+    }
+    const uint32_t nch = (len + 15) >> 4;
+    const uint32_t excl = wave_incl_scan(nch) - nch;
+    const uintptr_t addr = (uintptr_t)arena + 16ull * (tile_chunk[tile] + excl);
+    const uint32_t le_sum = ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len, nch, true, kflags);
+    if (valid) {
+        const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
+        const uint32_t P = pseudo ? Pbase + len : 0u;
+        if (VERIFY)
+            ok[seg] = fold16(P + F) == 0xFFFFu;
+        else
+            out[seg] = finish(P, F);
+    }
+}
+
+// Index of a packed batch: tile_chunk[t] for t = 0 .. ceil(n/64) (the last
+// entry = the arena's chunks).  Pass 1 sums each tile's chunks into
+// tile_chunk[t + 1]; pass 2, one block, turns them into a prefix in place.
+__global__ __launch_bounds__(64) void k_packed_tile_sums(const uint16_t* __restrict__ lens, uint64_t n,
+                                                         uint64_t* __restrict__ tile_chunk) {
+    const uint64_t seg = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const uint32_t nch = seg < n ? (lens[seg] + 15u) >> 4 : 0u;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(nch), 63);
+    if (threadIdx.x == 0) tile_chunk[blockIdx.x + 1] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_packed_tile_scan(uint64_t* __restrict__ tile_chunk, uint64_t n_tiles) {
+    __shared__ uint64_t part[1024];
+    const uint32_t i = threadIdx.x;
+    const uint64_t per = (n_tiles + 1023) / 1024, b = min<uint64_t>(n_tiles, i * per), e = min<uint64_t>(n_tiles, b + per);
+    uint64_t s = 0;
+    for (uint64_t k = b; k < e; k++) s += tile_chunk[k + 1];
+    part[i] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the 1024 partials
+        const uint64_t x = i >= off ? part[i - off] : 0ull;
+        __syncthreads();
+        part[i] += x;
+        __syncthreads();
+    }
+    // entries k+1 of this thread's range become inclusive prefixes (= the
+    // exclusive prefix of tile k+1); each thread touches only its own entries
+    uint64_t run = part[i] - s;
+    for (uint64_t k = b; k < e; k++) {
+        run += tile_chunk[k + 1];
+        tile_chunk[k + 1] = run;
+    }
+    if (i == 0) tile_chunk[0] = 0;
 }
 
 // Per packet: the segments' folded sums and lengths, packed by k_ragged as
@@ -1382,6 +1489,59 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
     return PIPCK_OK;
 }
 
+template <bool V, int U>
+static void launch_packed_u(bool nt, uint64_t tiles, hipStream_t s, const uint8_t* a, const uint16_t* lens,
+                            const uint64_t* tc, uint64_t n, const uint32_t* ps, uint32_t nf, const uint32_t* fo,
+                            uint64_t origin, uint16_t* out, uint8_t* ok, uint32_t f) {
+    if (nt)
+        hipLaunchKernelGGL((k_packed<V, U, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf, fo,
+                           origin, out, ok, f);
+    else
+        hipLaunchKernelGGL((k_packed<V, U, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf, fo,
+                           origin, out, ok, f);
+}
+
+static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
+                         uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                         uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, hipStream_t s) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_lens || !d_tile_chunk || (verify ? !d_ok : !d_out)) {
+        set_error("pipck_checksum_packed: null pointer");
+        return PIPCK_EINVAL;
+    }
+    if ((uintptr_t)d_arena % 16) {
+        set_error("pipck_checksum_packed: the arena must be 16-byte aligned");
+        return PIPCK_EINVAL;
+    }
+    if (d_pseudo && !d_flow_of && n_flows == 0) {
+        set_error("pipck_checksum_packed: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7FFFFFFFull) {
+        set_error("pipck_checksum_packed: more than 2^37 packets in one launch");
+        return PIPCK_ERANGE;
+    }
+    const uint32_t f = g_tune.flags.load();
+    const bool nt = nt_for(true);
+    const uint8_t* a = (const uint8_t*)d_arena;
+    const uint32_t nf = n_flows ? n_flows : 1u;
+    // rows in flight per wave: a ring of 24 by default (as k_ragged); 17/33 = 16/32
+    switch (g_tune.loads.load()) {
+        case 17: verify ? launch_packed_u<true, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
+                        : launch_packed_u<false, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+                 break;
+        case 33: verify ? launch_packed_u<true, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
+                        : launch_packed_u<false, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+                 break;
+        default: verify ? launch_packed_u<true, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
+                        : launch_packed_u<false, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+                 break;
+    }
+    PIPCK_LAUNCHED("k_packed");
+    return PIPCK_OK;
+}
+
 int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
                      const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo, uint32_t* d_scratch,
                      uint16_t* d_out, uint32_t* d_err, hipStream_t s) {
@@ -1467,6 +1627,40 @@ int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t 
         return PIPCK_EINVAL;
     }
     return launch_ragged(true, d_arena, d_desc, n, d_pseudo, nullptr, nullptr, d_ok, d_err, as_stream(stream));
+}
+
+int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
+                          const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
+                          uint16_t* d_out, void* stream) {
+    return launch_packed(false, d_arena, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out,
+                         nullptr, as_stream(stream));
+}
+
+int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
+                        const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
+                        uint8_t* d_ok, void* stream) {
+    return launch_packed(true, d_arena, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr,
+                         d_ok, as_stream(stream));
+}
+
+int pipck_packed_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_chunk, void* stream) {
+    if (!d_tile_chunk || (n && !d_lens)) {
+        set_error("pipck_packed_index: null pointer");
+        return PIPCK_EINVAL;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7FFFFFFFull) {
+        set_error("pipck_packed_index: more than 2^37 packets");
+        return PIPCK_ERANGE;
+    }
+    hipStream_t s = as_stream(stream);
+    if (tiles) {
+        hipLaunchKernelGGL(k_packed_tile_sums, dim3((uint32_t)tiles), dim3(64), 0, s, d_lens, n, d_tile_chunk);
+        PIPCK_LAUNCHED("k_packed_tile_sums");
+    }
+    hipLaunchKernelGGL(k_packed_tile_scan, dim3(1), dim3(1024), 0, s, d_tile_chunk, tiles);
+    PIPCK_LAUNCHED("k_packed_tile_scan");
+    return PIPCK_OK;
 }
 
 int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,

@@ -31,7 +31,10 @@ extern "C" {
  * tiny-stride flat kernel (8-B-multiple strides <= 64 B with pseudo-headers or
  * RX verify; loads_per_lane 4/8/16 = its ring, bits 8..15 its rows per wave
  * task, default 4 and 12), bit 18 = that kernel without pseudo-headers too, bits 24..27 =
- * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2). */
+ * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2), bit 19 = mixed rows of
+ * packed ragged tiles always find segments through LDS marks (default: a scalar
+ * loop over up to 4 segment ends per row).  The packed-batch kernel
+ * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 #ifdef __cplusplus

@@ -113,6 +113,59 @@ def verify_ragged(arena, desc, pseudo=None, ok=None, err=None):
     return ok
 
 
+def checksum_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
+                    flow_origin: int = 0, out=None):
+    """Packed ragged batch (pipck_checksum_packed): lens = device int16/uint16 tensor of
+    packet lengths, tile_chunk = packed_index(lens); packet i at 16 * (chunks before i)."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    _check_packed(arena, lens, tile_chunk, n)
+    call("pipck_checksum_packed", _ptr(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo), n_flows, _ptr(flow_of),
+         flow_origin, _ptr(out), current_stream(arena.device))
+    return out
+
+
+def verify_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
+                  flow_origin: int = 0, ok=None):
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check_packed(arena, lens, tile_chunk, n)
+    call("pipck_verify_packed", _ptr(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo), n_flows, _ptr(flow_of),
+         flow_origin, _ptr(ok), current_stream(arena.device))
+    return ok
+
+
+def packed_index(lens, n: int | None = None):
+    """tile_chunk for a packed batch: u64 (as int64) per 64 packets + the total."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    tc = torch.empty((n + 63) // 64 + 1, dtype=torch.int64, device=lens.device)
+    call("pipck_packed_index", _ptr(lens), n, _ptr(tc), current_stream(lens.device))
+    return tc
+
+
+_packed_ok: dict = {}
+
+
+def _check_packed(arena, lens, tile_chunk, n):
+    """Host-side guard (once per index tensor): the batch must lie inside the arena."""
+    if n > lens.numel() or tile_chunk.numel() < (n + 63) // 64 + 1:
+        raise ValueError("lens / tile_chunk shorter than the batch")
+    key = (tile_chunk.data_ptr(), n, arena.data_ptr(), arena.numel())
+    if key in _packed_ok:
+        return
+    chunks = int(tile_chunk[(n + 63) // 64].item())
+    if 16 * chunks > arena.numel() * arena.element_size():
+        raise ValueError(f"packed batch needs {16 * chunks} B, arena has {arena.numel() * arena.element_size()}")
+    if len(_packed_ok) > 64:
+        _packed_ok.clear()
+    _packed_ok[key] = True
+
+
 def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
     """segs: (n_segs, 2) int64 descriptors; seg_begin: (n_packets+1,) int64 CSR offsets."""
     torch = _torch()
@@ -185,15 +238,26 @@ def gen_ragged(n: int, first: int, seed: int, hdr: int, n_flows: int, device=Non
     return arena, desc, lengths
 
 
+def gen_packed(n: int, first: int, seed: int, hdr: int, device=None, lengths=None):
+    """Zipf-length batch (cfg4 shape) in the packed layout: (arena, lens u16-in-int16, tile_chunk, lengths i32).
+    Bytes and layout equal gen_ragged's; only the descriptors are replaced by lengths + a per-64 index."""
+    torch = _torch()
+    arena, desc, lengths = gen_ragged(n, first, seed, hdr, 1, device=device, lengths=lengths)
+    del desc
+    lens16 = lengths.to(torch.int16)
+    return arena, lens16, packed_index(lens16, n), lengths
+
+
 def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, plain_loads: bool = False,
          flat: bool = True, nt_loads: bool = False, rows_per_task: int = 0, xcd_groups: bool = False,
          packed_tiles: bool = True, wide_blocks: bool = False,
          small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True,
-         flat_tiny: bool = True, force_flat_tiny: bool = False) -> None:
+         flat_tiny: bool = True, force_flat_tiny: bool = False, packed_marks_only: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI."""
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
              | (0 if packed_tiles else 16) | (32 if wide_blocks else 0) | (0 if small else 64)
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
-             | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24))
+             | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
+             | (1 << 19 if packed_marks_only else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)

@@ -41,7 +41,8 @@ def test_pip_stack_on_amd_checksum_is_byte_identical(capture):
     assert r.returncode == 0, r.stderr[-2000:]
     want = GOLDEN.read_text().strip().splitlines()
     got = r.stdout.strip().splitlines()
-    assert got[-1] == want[-1]
+    extra = [ln[:120] for ln in got if ln not in want]
+    assert got[-1] == want[-1], (extra, [ln[:120] for ln in want if ln not in got])
     diff = [i for i, (a, b) in enumerate(zip(got, want)) if a != b]
     assert not diff and len(got) == len(want), diff[:5]
     # the deferred (batched) API on real pip_buf chains, flushed in one GPU batch

@@ -515,6 +515,107 @@ def test_ragged_packed_tiles(oracle, rows):
         engine.tune()
 
 
+def _packed_lens(rng, shape, n, oracle=None):
+    if shape == "zipf":
+        return oracle.zipf_lengths(4242, int(rng.integers(0, 1 << 30)), n)
+    lens = {
+        "uniform": lambda: rng.integers(0, 9001, n),
+        "tiny": lambda: rng.integers(0, 33, n),          # every tile <= 2 chunks: lane-per-packet path
+        "short": lambda: rng.integers(0, 120, n),        # many segment ends per row: the LDS-mark path
+        "mixed": lambda: np.where(rng.random(n) < 0.5, rng.integers(0, 80, n), rng.integers(0, 4000, n)),
+        "jumbo": lambda: rng.integers(30000, 65536, n),
+        "edge": lambda: rng.choice([0, 1, 2, 15, 16, 17, 31, 32, 33, 1023, 1024, 1025, 65534, 65535], n),
+    }[shape]()
+    return np.asarray(lens, dtype=np.uint32)
+
+
+def _packed_upload(rng, lens, misalign_padding=True):
+    """Host + device arena in the packed layout (padding bytes random, so every
+    tail mask matters); returns (host, offsets, arena, lens16, tile_chunk)."""
+    chunks = (lens.astype(np.uint64) + 15) // 16
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(chunks)[:-1] * 16
+    host = rng.integers(0, 256, int(chunks.sum()) * 16 + 16, dtype=np.uint8)
+    _, arena = upload(host, 0)
+    lens16 = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(DEV)
+    tc = engine.packed_index(lens16)
+    want_tc = np.concatenate([[0], np.cumsum(chunks)])[::64]
+    got_tc = tc.cpu().numpy()
+    assert np.array_equal(got_tc[:-1], want_tc[:len(got_tc) - 1]) and got_tc[-1] == chunks.sum()
+    return host, offs, arena, lens16, tc
+
+
+@pytest.mark.parametrize("shape", ["zipf", "uniform", "tiny", "short", "mixed", "jumbo", "edge"])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 3001])
+def test_packed_vs_oracle(oracle, shape, n):
+    """pipck_checksum_packed / pipck_verify_packed (lengths + a per-64 index,
+    no descriptors) against pip's algorithm, with implicit flows from an
+    origin, explicit flow indices and no pseudo-header; both mixed-row paths
+    (scalar end loop, LDS marks)."""
+    rng = np.random.default_rng(hash((shape, n)) % 2**32)
+    lens = _packed_lens(rng, shape, n, oracle)
+    host, offs, arena, lens16, tc = _packed_upload(rng, lens)
+    for fam, explicit in ((4, False), (6, True), (0, False)):
+        seed, proto, origin = 99 + n, 6 if fam == 4 else 17, int(rng.integers(0, 1 << 40))
+        pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+        flow_idx = (origin + np.arange(n)) % N_FLOWS
+        flow_of = None
+        if explicit:
+            flow_idx = rng.integers(0, N_FLOWS, n)
+            flow_of = torch.from_numpy(flow_idx.astype(np.int32)).to(DEV)
+        if fam == 0:
+            want = np.array([oracle.ip_checksum(host[int(o):int(o) + int(L)].tobytes()) for o, L in zip(offs, lens)],
+                            dtype=np.uint16)
+        elif explicit:
+            want = np.array([oracle.inet6_checksum(host[int(o):int(o) + int(L)].tobytes(), proto,
+                                                   *oracle.flow6(seed, int(f)), int(L))
+                             for o, L, f in zip(offs, lens, flow_idx)], dtype=np.uint16)
+        else:
+            want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
+        for marks in (False, True):
+            engine.tune(packed_marks_only=marks)
+            try:
+                got = u16(engine.checksum_packed(arena, lens16, tc, n, pseudo, N_FLOWS, flow_of,
+                                                 0 if explicit else origin))
+                ok = engine.verify_packed(arena, lens16, tc, n, pseudo, N_FLOWS, flow_of,
+                                          0 if explicit else origin).cpu().numpy().astype(bool)
+            finally:
+                engine.tune()
+            assert np.array_equal(got, want), (fam, marks, np.nonzero(got != want)[0][:5])
+            assert np.array_equal(ok, got == 0)
+
+
+@pytest.mark.parametrize("ring", [17, 25, 33])
+@pytest.mark.parametrize("nt", [False, True])
+def test_packed_rings_and_load_policy(oracle, ring, nt):
+    rng = np.random.default_rng(ring * 2 + nt)
+    n = 64 * 50 + 3
+    lens = _packed_lens(rng, "mixed", n)
+    host, offs, arena, lens16, tc = _packed_upload(rng, lens)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, 5, 6)
+    engine.tune(0, ring, plain_loads=not nt, nt_loads=nt)
+    try:
+        got = u16(engine.checksum_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 7))
+    finally:
+        engine.tune()
+    assert np.array_equal(got, oracle.batch_ragged(host, offs, lens, 4, 6, 5, N_FLOWS, 7))
+
+
+def test_packed_argument_checks():
+    lens16 = torch.zeros(10, dtype=torch.int16, device=DEV)
+    tc = engine.packed_index(lens16)
+    arena = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    lib = _lib.load()
+    out = torch.empty(10, dtype=torch.int16, device=DEV)
+    rc = lib.pipck_checksum_packed(C.c_void_p(arena.data_ptr() + 1), C.c_void_p(lens16.data_ptr()),
+                                   C.c_void_p(tc.data_ptr()), 10, None, 1, None, 0, C.c_void_p(out.data_ptr()), None)
+    assert rc == _lib.PIPCK_EINVAL  # misaligned arena
+    with pytest.raises(ValueError):  # the index says more bytes than the arena holds
+        big = torch.full((10,), 100, dtype=torch.int16, device=DEV)
+        engine.checksum_packed(arena, big, engine.packed_index(big))
+
+
 @pytest.mark.parametrize("misalign", [0, 3, 8])
 def test_ragged_tiny_segment_tiles(oracle, misalign):
     """Tiles whose segments all span <= 2 chunks take the lane-per-segment path
@@ -732,6 +833,36 @@ def test_full_size_ragged(oracle):
     ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy()
     assert not ok[::5].any() and ok[np.arange(n) % 5 != 0].all()
     del arena, desc, out, again
+    torch.cuda.empty_cache()
+
+
+def test_full_size_packed(oracle):
+    """cfg4 at its BASELINE size through the packed-lengths ABI (the bench's
+    path): equal to the descriptor kernel on the same arena, sampled against
+    the oracle, and checksum-of-checksum over the whole batch."""
+    w, n = CFG4, 8 << 20
+    arena, lens16, tc, lens = engine.gen_packed(n, 0, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    out = engine.checksum_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 0)
+    got = u16(out)
+    L = lens.cpu().numpy().astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum((L.astype(np.uint64) + 15) // 16)[:-1] * 16
+    desc = engine.make_desc(offs, L, np.arange(n) % N_FLOWS)
+    assert np.array_equal(got, u16(engine.checksum_ragged(arena, desc, pseudo)))
+    del desc
+    rng = np.random.default_rng(44)
+    for i in rng.choice(n, 1500, replace=False):
+        pkt = oracle.packet(w.seed, int(i), int(L[i]), w.hdr)
+        assert got[i] == oracle.inet_checksum(pkt, w.proto, *oracle.flow4(w.seed, int(i) % N_FLOWS)), int(i)
+    o = torch.from_numpy(offs.astype(np.int64)).to(DEV) + 16
+    v = out.to(torch.int32) & 0xFFFF
+    arena[o] = (v >> 8).to(torch.uint8)
+    arena[o + 1] = (v & 0xFF).to(torch.uint8)
+    again = engine.checksum_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 0)
+    assert int((again != 0).sum().item()) == 0
+    assert bool((engine.verify_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 0) == 1).all())
+    del arena, out, again
     torch.cuda.empty_cache()
 
 

@@ -70,8 +70,10 @@ def main() -> None:
     avg_ns = float(top["AverageNs"])
     traffic = {"workload": wl, "tag": tag, "kernel": kname, "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
                "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": algo,
+               "arena_stride": bench["config"]["arena_stride"], "packets": bench["config"]["packets_per_gpu"],
                "traffic_over_algorithmic": round(hbm / algo, 4), "rocprof_avg_ns": avg_ns,
                "bench_event_kernel_ms": bench["roofline"]["kernel_ms"],
+               "rocprof_vs_bench_event": round(avg_ns / 1e6 / bench["roofline"]["kernel_ms"], 4),
                "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts 1/2 of wide streams)"}
     (prof / f"traffic_{wl}.json").write_text(json.dumps(traffic, indent=1) + "\n")
     md = [f"# {tag} {wl}: rocprofv3 summary", "",
@@ -82,7 +84,8 @@ def main() -> None:
         md.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                   f"{float(r['Percentage']):.2f}% |")
     md += ["", f"Dominant kernel: `{kname[:120]}`", "",
-           f"* rocprof average duration {avg_ns / 1e6:.4f} ms vs bench HIP-event mean {bench['roofline']['kernel_ms']} ms",
+           f"* rocprof average duration {avg_ns / 1e6:.4f} ms vs bench per-dispatch HIP-event median "
+           f"{bench['roofline']['kernel_ms']} ms (back-to-back mean {bench['roofline'].get('kernel_ms_b2b_mean')} ms)",
            f"* algorithmic bytes per launch {algo:,} (L + 2 per packet)",
            f"* FETCH_SIZE {fetch_kb:,.0f} KB, WRITE_SIZE {write_kb:,.0f} KB per launch",
            f"* HBM bytes per launch (2 x FETCH + WRITE) {hbm:,.0f} = {hbm / algo:.3f} x algorithmic",
