@@ -69,10 +69,9 @@ class PcAdapter:
 @pytest.fixture
 def staged_per_packet():
     """The per-packet path with staged copies (the default auto mode zero-copies small calls)."""
-    lib = _lib.load()
-    checksum.set_zero_copy(0)
+    pc.set_zero_copy(0)
     yield
-    checksum.set_zero_copy(2)
+    pc.set_zero_copy(2)
 
 
 def test_every_known_answer_on_gpu(kat, staged_per_packet):
@@ -87,13 +86,12 @@ def test_every_known_answer_on_gpu(kat, staged_per_packet):
 def test_every_known_answer_on_gpu_zero_copy(kat):
     """The same known answers through the zero-copy per-packet path (the kernel
     reads pinned host staging and writes the result to host memory)."""
-    lib = _lib.load()
-    checksum.set_zero_copy(1)
+    pc.set_zero_copy(1)
     try:
         bad = [c["fn"] for c in kat if run_case(PcAdapter, c) != c["expect"]]
         assert not bad, bad[:5]
     finally:
-        checksum.set_zero_copy(2)
+        pc.set_zero_copy(2)
 
 
 def test_per_packet_api_is_thread_safe(kat):
