@@ -75,7 +75,10 @@ def main() -> None:
                "bench_event_kernel_ms": bench["roofline"]["kernel_ms"],
                "rocprof_vs_bench_event": round(avg_ns / 1e6 / bench["roofline"]["kernel_ms"], 4),
                "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts 1/2 of wide streams)"}
-    (prof / f"traffic_{wl}.json").write_text(json.dumps(traffic, indent=1) + "\n")
+    # a tag with a size suffix (TAG=r02_268435456) profiles a non-default batch size:
+    # keep it beside, not over, the default-size traffic file bench.py reads
+    sfx = f"_{tag.split('_', 1)[1]}" if "_" in tag else ""
+    (prof / f"traffic_{wl}{sfx}.json").write_text(json.dumps(traffic, indent=1) + "\n")
     md = [f"# {tag} {wl}: rocprofv3 summary", "",
           f"Command: `tools/profile.sh` (TAG={tag} WL={wl}) on one MI355X; bench line of the trace pass:", "",
           "```", json.dumps(bench), "```", "",
