@@ -1,0 +1,244 @@
+// stack_tx_bench.cpp -- MEASUREMENT / TEST INFRASTRUCTURE.
+//
+// pip's TCP transmit path at volume: pip_tcp::write (pip/protocol/pip_tcp_public.cpp:43-48
+// -> pip_tcp::_write, pip/protocol/pip_tcp_private.cpp:74-120) cuts the caller's buffer
+// into MSS segments; every segment's TCP checksum is taken inside pip_tcp_packet's
+// constructor (pip/protocol/pip_tcp_packet.cpp:124-134) and every IPv4 header's inside
+// pip_netif::output4 (pip/pip_netif.cpp:94-97).  A scripted peer completes the handshake
+// (MSS option + window scale 14, so pip's send window is 1 GiB) and ACKs every write(),
+// which ends in a PUSH pip waits on (pip_tcp_private.cpp:99-107, 121-128, 211-226).
+//
+// Linked three ways by oracle/Makefile (pip's stack compiled from /root/reference):
+//   _ref/stack_tx_ref : pip's own pip_checksum.cpp                      --mode ref
+//   _ref/stack_tx_amd : the stack WITHOUT pip_checksum.o + libpip_checksum_amd.so
+//        --mode sync        every checksum call runs on the GPU as it is made (unchanged pip)
+//        --mode capture     the drop-in's capture mode: pip's unchanged call sites queue
+//                           their checksums; the output callback holds each packet; one
+//                           pip_checksum_amd_flush() per write() fills every field, then
+//                           the packets go out
+//        --mode capture_zc  the same, with the write() buffer in pinned memory
+//                           (pipck_host_alloc) and pip_checksum_amd_zero_copy(true): the
+//                           GPU reads the payload segments in place
+//
+// Output (one JSON line): payload GiB/s and packets/s through the whole TX path, and a
+// digest of every emitted packet -- with --verify, FNV-1a over every wire byte; else over
+// each packet's IPv4 and TCP checksum fields and length -- which must be equal across the
+// three builds/modes for the same arguments.
+#include "pip_netif.h"
+#include "pip_checksum.h"
+#include "protocol/pip_tcp.h"
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unistd.h>
+#include <vector>
+
+#ifdef PIPCK_AMD
+#include "pip_checksum_amd.h"
+#include "pipck.h"
+#endif
+
+namespace {
+
+enum Mode { REF, SYNC, CAPTURE, CAPTURE_ZC };
+
+Mode g_mode = REF;
+bool g_verify = false;
+bool g_hold = false;  // capture modes: packets wait for the flush
+std::shared_ptr<pip_tcp> g_tcp;
+std::vector<std::vector<std::shared_ptr<pip_buf>>> g_pending;
+uint64_t g_digest = 1469598103934665603ull;
+uint64_t g_packets = 0, g_wire_bytes = 0;
+uint32_t g_srv_next = 0;  // pip's next sequence number, from the emitted segments
+
+inline void fnv(const uint8_t* p, size_t n) {
+    uint64_t h = g_digest;
+    for (size_t i = 0; i < n; i++) h = (h ^ p[i]) * 1099511628211ull;
+    g_digest = h;
+}
+
+// an emitted packet: IPv4 header segment -> TCP header segment -> payload segment(s)
+void emit(const std::vector<std::shared_ptr<pip_buf>>& segs) {
+    size_t len = 0;
+    for (auto& s : segs) len += s->payload_len();
+    if (g_verify) {
+        for (auto& s : segs) fnv((const uint8_t*)s->payload(), s->payload_len());
+    } else {
+        const uint8_t* ip = (const uint8_t*)segs[0]->payload();
+        uint8_t rec[8] = {ip[10], ip[11], 0, 0, (uint8_t)len, (uint8_t)(len >> 8), 0, 0};
+        if (segs.size() > 1 && segs[1]->payload_len() >= 18) {
+            const uint8_t* th = (const uint8_t*)segs[1]->payload();
+            rec[2] = th[16];
+            rec[3] = th[17];
+        }
+        fnv(rec, sizeof rec);
+    }
+    if (segs.size() > 1 && segs[1]->payload_len() >= 8) {
+        const uint8_t* th = (const uint8_t*)segs[1]->payload();
+        const uint32_t seq = (uint32_t)th[4] << 24 | (uint32_t)th[5] << 16 | (uint32_t)th[6] << 8 | th[7];
+        size_t data = 0;
+        for (size_t i = 2; i < segs.size(); i++) data += segs[i]->payload_len();
+        g_srv_next = seq + (uint32_t)data + ((th[13] & (TH_SYN | TH_FIN)) ? 1 : 0);
+    }
+    g_packets++;
+    g_wire_bytes += len;
+}
+
+void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
+    std::vector<std::shared_ptr<pip_buf>> segs;
+    for (auto q = buf; q; q = q->next()) segs.push_back(q);
+    if (g_hold)
+        g_pending.push_back(std::move(segs));
+    else
+        emit(segs);
+}
+
+// after each stack action: capture modes store every queued field, then output the packets
+void settle() {
+#ifdef PIPCK_AMD
+    if (!g_hold) return;
+    pip_checksum_amd_flush();
+    for (auto& s : g_pending) emit(s);
+    g_pending.clear();
+#endif
+}
+
+void on_connect(pip_netif&, std::shared_ptr<pip_tcp> tcp, const void* hs, pip_uint16) {
+    g_tcp = tcp;
+    tcp->connected(hs);
+}
+
+void put16(uint8_t* p, uint16_t v) { p[0] = v >> 8; p[1] = (uint8_t)v; }
+void put32(uint8_t* p, uint32_t v) { put16(p, v >> 16); put16(p + 2, (uint16_t)v); }
+
+// a client segment to pip (10.0.0.2:40000 -> 10.0.0.1:80); RX takes no checksum
+std::vector<uint8_t> craft(uint32_t seq, uint32_t ack, uint8_t flags, const std::vector<uint8_t>& opts) {
+    const size_t thl = 20 + opts.size();
+    std::vector<uint8_t> p(20 + thl, 0);
+    p[0] = 0x45;
+    put16(&p[2], (uint16_t)p.size());
+    p[8] = 64;
+    p[9] = IPPROTO_TCP;
+    const uint8_t cli[4] = {10, 0, 0, 2}, srv[4] = {10, 0, 0, 1};
+    memcpy(&p[12], cli, 4);
+    memcpy(&p[16], srv, 4);
+    uint8_t* t = &p[20];
+    put16(t, 40000);
+    put16(t + 2, 80);
+    put32(t + 4, seq);
+    put32(t + 8, ack);
+    t[12] = (uint8_t)((thl / 4) << 4);
+    t[13] = flags;
+    put16(t + 14, 65535);  // << 14 (the SYN's window-scale option): a 1 GiB send window
+    memcpy(t + 20, opts.data(), opts.size());
+    return p;
+}
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    std::string mode = "ref";
+    unsigned mss = 1460;
+    size_t total = 256ull << 20, per_write = 4ull << 20;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto val = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+        if (a == "--mode") mode = val();
+        else if (a == "--mss") mss = (unsigned)atoi(val());
+        else if (a == "--bytes") total = strtoull(val(), nullptr, 0);
+        else if (a == "--write") per_write = strtoull(val(), nullptr, 0);
+        else if (a == "--verify") g_verify = true;
+        else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
+    }
+    if (mode == "ref") g_mode = REF;
+    else if (mode == "sync") g_mode = SYNC;
+    else if (mode == "capture") g_mode = CAPTURE;
+    else if (mode == "capture_zc") g_mode = CAPTURE_ZC;
+    else { fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
+#ifndef PIPCK_AMD
+    if (g_mode != REF) { fprintf(stderr, "this build links pip's own pip_checksum.cpp: --mode ref only\n"); return 2; }
+#else
+    if (g_mode == REF) { fprintf(stderr, "this build links libpip_checksum_amd.so: sync/capture/capture_zc\n"); return 2; }
+#endif
+    if (mss < 1 || mss > 65495 || per_write < 1 || per_write > (1u << 30)) {
+        fprintf(stderr, "bad --mss / --write\n");
+        return 2;
+    }
+
+    // the application's send buffer: pip's pip_buf points into it (write(..., is_copy=false))
+    uint8_t* buf = nullptr;
+#ifdef PIPCK_AMD
+    if (g_mode == CAPTURE_ZC) buf = (uint8_t*)pipck_host_alloc(per_write);
+#endif
+    std::vector<uint8_t> plain;
+    if (!buf) {
+        plain.resize(per_write);
+        buf = plain.data();
+    }
+    for (size_t i = 0; i < per_write; i++) buf[i] = (uint8_t)(i * 131 + (i >> 11) * 7 + 1);
+
+    uint8_t z[20] = {0};
+    (void)pip_ip_checksum(z, 20);  // one-time GPU initialisation before pip's clocks run
+#ifdef PIPCK_AMD
+    if (g_mode == CAPTURE || g_mode == CAPTURE_ZC) {
+        pip_checksum_amd_capture(true);
+        if (g_mode == CAPTURE_ZC) pip_checksum_amd_zero_copy(true);
+        g_hold = true;
+        pip_ip_checksum(z, 20);  // warm this thread's TX queue
+        pip_checksum_amd_flush();
+    }
+#endif
+    auto& nif = pip_netif::shared();
+    nif.output_ip_data_callback = on_output;
+    nif.new_tcp_connect_callback = on_connect;
+
+    uint32_t cseq = 7000;
+    const std::vector<uint8_t> opts = {2, 4, (uint8_t)(mss >> 8), (uint8_t)mss, 3, 3, 14, 1};
+    auto syn = craft(cseq, 0, TH_SYN, opts);
+    nif.input(syn.data());
+    settle();
+    if (!g_tcp) { fprintf(stderr, "no connection\n"); return 1; }
+    cseq += 1;
+    auto ack = craft(cseq, g_srv_next, TH_ACK, {});
+    nif.input(ack.data());
+    settle();
+
+    const uint64_t pk0 = g_packets;
+    size_t sent = 0;
+    unsigned writes = 0;
+    const double t0 = now();
+    while (sent < total) {
+        const size_t want = total - sent < per_write ? total - sent : per_write;
+        const uint32_t w = g_tcp->write(buf, (pip_uint32)want, false);
+        settle();
+        if (w == 0) { fprintf(stderr, "write stalled at %zu bytes\n", sent); return 1; }
+        sent += w;
+        writes++;
+        auto a = craft(cseq, g_srv_next, TH_ACK, {});  // the peer ACKs the whole write (and its PUSH)
+        nif.input(a.data());
+        settle();
+    }
+    const double el = now() - t0;
+    const uint64_t pk = g_packets - pk0;
+#ifdef PIPCK_AMD
+    if (g_hold) {
+        pip_checksum_amd_zero_copy(false);
+        pip_checksum_amd_capture(false);
+    }
+#endif
+    printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
+           "\"writes\": %u, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
+           "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu}\n",
+           mode.c_str(), mss, per_write, sent, writes, (unsigned long long)pk, el, sent / el / (1u << 30),
+           pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
+           (unsigned long long)g_wire_bytes);
+    fflush(stdout);
+    _exit(0);  // pip's timer thread is detached and never stops
+}
