@@ -19,6 +19,8 @@
 //        --mode capture_zc  the same, with the write() buffer in pinned memory
 //                           (pipck_host_alloc) and pip_checksum_amd_zero_copy(true): the
 //                           GPU reads the payload segments in place
+//   _ref/stack_tx_zero: every checksum returns 0 (oracle/ck_zero.cpp)    --mode zero
+//        pip's TX path with no checksum work: the ceiling of any offload (wrong wire bytes)
 //
 // Output (one JSON line): payload GiB/s and packets/s through the whole TX path, and a
 // digest of every emitted packet -- with --verify, FNV-1a over every wire byte; else over
@@ -28,11 +30,13 @@
 #include "pip_checksum.h"
 #include "protocol/pip_tcp.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <unistd.h>
 #include <vector>
 
@@ -43,7 +47,7 @@
 
 namespace {
 
-enum Mode { REF, SYNC, CAPTURE, CAPTURE_ZC };
+enum Mode { REF, SYNC, CAPTURE, CAPTURE_ZC, ZERO };
 
 Mode g_mode = REF;
 bool g_verify = false;
@@ -53,6 +57,7 @@ std::vector<std::vector<std::shared_ptr<pip_buf>>> g_pending;
 uint64_t g_digest = 1469598103934665603ull;
 uint64_t g_packets = 0, g_wire_bytes = 0;
 uint32_t g_srv_next = 0;  // pip's next sequence number, from the emitted segments
+FILE* g_dump = nullptr;   // --dump: one 12-byte record per packet (seq, ip_id, ip_sum, th_sum, length)
 
 inline void fnv(const uint8_t* p, size_t n) {
     uint64_t h = g_digest;
@@ -83,11 +88,31 @@ void emit(const std::vector<std::shared_ptr<pip_buf>>& segs) {
         for (size_t i = 2; i < segs.size(); i++) data += segs[i]->payload_len();
         g_srv_next = seq + (uint32_t)data + ((th[13] & (TH_SYN | TH_FIN)) ? 1 : 0);
     }
+    if (g_dump) {
+        const uint8_t* ip = (const uint8_t*)segs[0]->payload();
+        uint8_t rec[12] = {0};
+        if (segs.size() > 1 && segs[1]->payload_len() >= 18) memcpy(rec, (const uint8_t*)segs[1]->payload() + 4, 4);
+        rec[4] = ip[4], rec[5] = ip[5], rec[6] = ip[10], rec[7] = ip[11];
+        if (segs.size() > 1 && segs[1]->payload_len() >= 18)
+            rec[8] = ((const uint8_t*)segs[1]->payload())[16], rec[9] = ((const uint8_t*)segs[1]->payload())[17];
+        rec[10] = (uint8_t)(len >> 8), rec[11] = (uint8_t)len;
+        fwrite(rec, 1, sizeof rec, g_dump);
+    }
     g_packets++;
     g_wire_bytes += len;
 }
 
+std::thread::id g_main;
+std::atomic<uint64_t> g_retransmits{0};
+
 void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
+    // pip's timer thread resends a segment left unacknowledged for 1 s
+    // (pip/protocol/pip_tcp_check.cpp:25-39); it never should here, and a run where
+    // it did is reported as invalid rather than digested
+    if (std::this_thread::get_id() != g_main) {
+        g_retransmits++;
+        return;
+    }
     std::vector<std::shared_ptr<pip_buf>> segs;
     for (auto q = buf; q; q = q->next()) segs.push_back(q);
     if (g_hold)
@@ -155,14 +180,18 @@ int main(int argc, char** argv) {
         else if (a == "--bytes") total = strtoull(val(), nullptr, 0);
         else if (a == "--write") per_write = strtoull(val(), nullptr, 0);
         else if (a == "--verify") g_verify = true;
+        else if (a == "--dump") g_dump = fopen(val(), "wb");
         else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }
     if (mode == "ref") g_mode = REF;
     else if (mode == "sync") g_mode = SYNC;
     else if (mode == "capture") g_mode = CAPTURE;
     else if (mode == "capture_zc") g_mode = CAPTURE_ZC;
+    else if (mode == "zero") g_mode = ZERO;
     else { fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
-#ifndef PIPCK_AMD
+#if defined(PIPCK_ZERO)
+    if (g_mode != ZERO) { fprintf(stderr, "this build links checksums that return 0: --mode zero only\n"); return 2; }
+#elif !defined(PIPCK_AMD)
     if (g_mode != REF) { fprintf(stderr, "this build links pip's own pip_checksum.cpp: --mode ref only\n"); return 2; }
 #else
     if (g_mode == REF) { fprintf(stderr, "this build links libpip_checksum_amd.so: sync/capture/capture_zc\n"); return 2; }
@@ -184,15 +213,29 @@ int main(int argc, char** argv) {
     }
     for (size_t i = 0; i < per_write; i++) buf[i] = (uint8_t)(i * 131 + (i >> 11) * 7 + 1);
 
+    g_main = std::this_thread::get_id();
+    // One-time GPU initialisation (device, streams, every kernel the calls below
+    // reach, pinned staging) before pip's 1 s retransmit clock runs: a first flush
+    // that loads its kernels during the handshake can outlast it.
     uint8_t z[20] = {0};
-    (void)pip_ip_checksum(z, 20);  // one-time GPU initialisation before pip's clocks run
+    struct in_addr a4;
+    a4.s_addr = 0x0100000a;
+    auto warm = [&]() {
+        auto head = std::make_shared<pip_buf>(20);
+        head->set_next(std::make_shared<pip_buf>(buf, (pip_uint32)(per_write < 1460 ? per_write : 1460), 0));
+        (void)pip_ip_checksum(z, 20);
+        (void)pip_inet_checksum_buf(head, IPPROTO_TCP, a4, a4);
+    };
+    warm();
 #ifdef PIPCK_AMD
     if (g_mode == CAPTURE || g_mode == CAPTURE_ZC) {
         pip_checksum_amd_capture(true);
         if (g_mode == CAPTURE_ZC) pip_checksum_amd_zero_copy(true);
         g_hold = true;
-        pip_ip_checksum(z, 20);  // warm this thread's TX queue
-        pip_checksum_amd_flush();
+        for (int i = 0; i < 2; i++) {  // warm this thread's TX queue (both double-buffered batches)
+            warm();
+            pip_checksum_amd_flush();
+        }
     }
 #endif
     auto& nif = pip_netif::shared();
@@ -235,10 +278,11 @@ int main(int argc, char** argv) {
 #endif
     printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
            "\"writes\": %u, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
-           "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu}\n",
+           "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu}\n",
            mode.c_str(), mss, per_write, sent, writes, (unsigned long long)pk, el, sent / el / (1u << 30),
            pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
-           (unsigned long long)g_wire_bytes);
+           (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load());
     fflush(stdout);
-    _exit(0);  // pip's timer thread is detached and never stops
+    if (g_dump) fclose(g_dump);
+    _exit(g_retransmits.load() ? 3 : 0);  // pip's timer thread is detached and never stops
 }
