@@ -334,19 +334,33 @@ static void deferred_check_zero_copy() {
 #endif
 
 int main() {
-    // Touch the checksum provider once so any one-time initialisation happens
-    // before pip's 1 s retransmit clock starts on the first queued segment.
+    // Touch every checksum path once (IPv4 header, TCP/UDP chains over v4 and
+    // v6) so one-time initialisation -- device, streams, pinned staging, the
+    // first launch of each kernel -- happens before pip's 1 s retransmit clock
+    // starts on the first queued segment; a first flush that loads its kernels
+    // mid-handshake can outlast it and make pip resend the SYN-ACK.
     uint8_t z[20] = {0};
-    (void)pip_ip_checksum(z, 20);
+    std::vector<uint8_t> body(1460, 0x5a);
+    auto warm = [&]() {
+        auto head = std::make_shared<pip_buf>(20);
+        head->set_next(std::make_shared<pip_buf>(body.data(), (pip_uint32)body.size(), 0));
+        struct in_addr a4;
+        a4.s_addr = 0x0100000a;
+        struct in6_addr a6 = {};
+        (void)pip_ip_checksum(z, 20);
+        (void)pip_inet_checksum_buf(head, IPPROTO_TCP, a4, a4);
+        (void)pip_inet6_checksum_buf(head, IPPROTO_UDP, a6, a6);
+    };
+    warm();
 
 #ifdef PIPCK_DEFERRED_CHECK
     if (getenv("PIPCK_REPLAY_CAPTURE")) {
         pip_checksum_amd_capture(true);
         g_capture = true;
-        // warm the thread's TX queue (stream, pinned staging, kernels) so the first
-        // real flush does not stretch a session past pip's 1 s retransmit timer
-        pip_ip_checksum(z, 20);
-        pip_checksum_amd_flush();
+        for (int i = 0; i < 2; i++) {  // both of the queue's double-buffered batches
+            warm();
+            pip_checksum_amd_flush();
+        }
     }
 #endif
     auto& nif = pip_netif::shared();

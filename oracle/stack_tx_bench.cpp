@@ -226,15 +226,20 @@ int main(int argc, char** argv) {
         (void)pip_ip_checksum(z, 20);
         (void)pip_inet_checksum_buf(head, IPPROTO_TCP, a4, a4);
     };
+    double cold[3] = {0, 0, 0};  // seconds: first synchronous calls, first and second capture flush
+    double tw = now();
     warm();
+    cold[0] = now() - tw;
 #ifdef PIPCK_AMD
     if (g_mode == CAPTURE || g_mode == CAPTURE_ZC) {
         pip_checksum_amd_capture(true);
         if (g_mode == CAPTURE_ZC) pip_checksum_amd_zero_copy(true);
         g_hold = true;
         for (int i = 0; i < 2; i++) {  // warm this thread's TX queue (both double-buffered batches)
+            tw = now();
             warm();
             pip_checksum_amd_flush();
+            cold[1 + i] = now() - tw;
         }
     }
 #endif
@@ -278,10 +283,12 @@ int main(int argc, char** argv) {
 #endif
     printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
            "\"writes\": %u, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
-           "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu}\n",
+           "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu, "
+           "\"cold_ms\": {\"first_calls\": %.3f, \"first_flush\": %.3f, \"second_flush\": %.3f}}\n",
            mode.c_str(), mss, per_write, sent, writes, (unsigned long long)pk, el, sent / el / (1u << 30),
            pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
-           (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load());
+           (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load(), cold[0] * 1e3, cold[1] * 1e3,
+           cold[2] * 1e3);
     fflush(stdout);
     if (g_dump) fclose(g_dump);
     _exit(g_retransmits.load() ? 3 : 0);  // pip's timer thread is detached and never stops

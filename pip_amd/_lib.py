@@ -92,6 +92,7 @@ SIGNATURES = {
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only
 INTERNAL_SIGNATURES = {
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
+    "pipck_trace_tasks": (_i32, [_p, _u64]),
 }
 
 _lib = None

@@ -106,4 +106,21 @@ __device__ __forceinline__ const global_u32x4* as_global(const u32x4* p) { retur
 __device__ __forceinline__ u32x4 load_stream(const u32x4* p) { return __builtin_nontemporal_load(as_global(p)); }
 __device__ __forceinline__ u32x4 load_plain(const u32x4* p) { return *as_global(p); }
 
+// Range-checked 16-byte loads through a raw buffer resource (base, bytes): a
+// lane whose offset reaches `bytes` gets zeros and sends NO memory request.
+// The streaming kernels keep every row load unconditional (so each row waits
+// for itself alone, vmcnt(U-1)); past a task's end those loads used to be
+// clamped onto its last chunk, and with ~7 MB in flight per XCD against a 4 MB
+// L2 that line was often gone again, so each clamped load could fetch 128 B
+// once more.  Range checking covers the VGPR offset only (not soffset), so
+// the row is part of the per-lane offset.
+typedef __amdgpu_buffer_rsrc_t buf_t;
+__device__ __forceinline__ buf_t buf_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+template <bool NT>
+__device__ __forceinline__ u32x4 buf_load(buf_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT ? 2 : 0);  // aux bit 1 = nt (gfx94x/950)
+}
+
 }  // namespace pipck

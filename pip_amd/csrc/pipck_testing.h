@@ -37,6 +37,13 @@ extern "C" {
  * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
+/* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the
+ * flat-stream (k_flat) and packed ragged (k_packed) kernels store one record
+ * {u64 task, u64 t_start, u64 t_end, u64 XCC_ID << 32 | HW_ID} per wave task
+ * (100 MHz s_memrealtime clock) into d_buf[task] for task < cap.  d_buf is
+ * device memory; null switches recording off. */
+int pipck_trace_tasks(void* d_buf, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-WORKLOADS = {"cfg1": 256 << 20, "cfg1p": 256 << 20, "cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20}
+WORKLOADS = {"cfg1": 256 << 20, "cfg1p": 256 << 20, "cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20,
+             "cfg4d": 8 << 20}
 
 
 def worker(only: list[str], iters: int) -> None:
@@ -41,7 +42,11 @@ def worker(only: list[str], iters: int) -> None:
         w, n = BY_CFG[int(name[3:4])], WORKLOADS[name]
         fam = w.family or (4 if name.endswith("p") else 0)  # cfg1p: cfg1 with IPv4 pseudo-headers
         pseudo = engine.gen_flows(fam, N_FLOWS, w.seed, w.proto or 6)[1] if fam else None
-        if w.ragged:
+        if w.ragged and not name.endswith("d"):  # cfg4: the packed layout bench.py runs
+            arena, lens16, tile_chunk, lens = engine.gen_packed(n, 0, w.seed, w.hdr)
+            nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
+            run = lambda: engine.checksum_packed(arena, lens16, tile_chunk, n, pseudo, N_FLOWS)  # noqa: E731
+        elif w.ragged:  # cfg4d: 16-byte descriptors (pipck_checksum_ragged)
             arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
             run = lambda: engine.checksum_ragged(arena, desc, pseudo)  # noqa: E731

@@ -1,0 +1,6 @@
+set -u
+mkdir -p gpurun_out/trace gpurun_out/scan
+timeout -k 10 300 python3 tools/size_scan.py --only cfg2,cfg3 --sizes 4 --arms '{"default": {}, "queue": {"flat_queue": true}}' > gpurun_out/scan/queue.jsonl 2> gpurun_out/scan/queue.err || exit 1
+timeout -k 10 300 python3 tools/size_scan.py --only cfg2 --arms '{"default": {}, "queue": {"flat_queue": true}}' >> gpurun_out/scan/queue.jsonl 2>> gpurun_out/scan/queue.err || exit 1
+timeout -k 10 300 python3 tools/size_scan.py --only cfg5 --sizes 8 --arms '{"default": {}, "queue": {"flat_queue": true}}' >> gpurun_out/scan/queue.jsonl 2>> gpurun_out/scan/queue.err || exit 1
+timeout -k 10 400 python3 tools/task_trace.py --only cfg2,cfg3 --arms '{"default": {}, "queue": {"flat_queue": true}}' --dump gpurun_out/trace/npyq > gpurun_out/trace/trace_queue.jsonl 2> gpurun_out/trace/traceq.err
