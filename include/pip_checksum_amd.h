@@ -70,6 +70,13 @@ void pip_checksum_amd_complete();
 // then, and the pinned range cannot be freed meanwhile (PIPCK_EBUSY).
 void pip_checksum_amd_zero_copy(bool on);
 
+// Resident per-call service for this thread (pipck_ctx_zero_copy mode 3,
+// include/pipck.h): pip's synchronous calls are answered by a GPU block that
+// stays resident and polls a doorbell instead of a kernel launch per call.  The
+// block exits after 50 ms without a call and restarts on the next one.  Off by
+// default (auto mode); PIPCK_HOST_ZERO_COPY=3 turns it on for new threads.
+void pip_checksum_amd_resident(bool on);
+
 // Capture mode for this thread: pip's UNCHANGED TX call sites become queue
 // entries.  While on, the three calls pip's TX path makes --
 //   pip_ip_checksum(hdr, len >= 20)            ip_sum  at hdr + 10  (pip_netif.cpp:94-97)

@@ -214,9 +214,13 @@ int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stri
 /* This context's per-packet path (pipck_host_sum): 0 = staged (H2D copy,
  * kernel, D2H copy), 1 = zero-copy (the kernel reads the pinned, coherent
  * staging buffer and writes the result to pinned host memory), 2 = auto
- * (zero-copy up to 64 KiB of staged bytes).  A new context starts in the mode
- * the environment variable PIPCK_HOST_ZERO_COPY (0/1/2) names, default 2.
- * Either path computes the same result. */
+ * (zero-copy up to 64 KiB of staged bytes), 3 = resident (up to 64 KiB: one
+ * 256-thread block of this context stays on the GPU, polls a doorbell in
+ * pinned host memory and answers without a launch; it exits after 50 ms
+ * without a call, or when the mode changes or the context is destroyed, and
+ * relaunches on the next call; larger calls take the zero-copy launch).  A new
+ * context starts in the mode the environment variable PIPCK_HOST_ZERO_COPY
+ * (0..3) names, default 2.  Every path computes the same result. */
 int pipck_ctx_zero_copy(pipck_ctx* ctx, int mode);
 void* pipck_host_alloc(size_t bytes);   /* pinned, coherent host memory (device-readable in place) */
 /* Pin an existing host range (a utun / socket buffer ring) so the GPU can read

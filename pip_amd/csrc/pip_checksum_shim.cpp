@@ -238,6 +238,11 @@ void pip_checksum_amd_zero_copy(bool on) {
     t_ctx.zero_copy = on;
 }
 
+void pip_checksum_amd_resident(bool on) {
+    int rc = pipck_ctx_zero_copy(t_ctx.get(), on ? 3 : 2);
+    if (rc) die("pipck_ctx_zero_copy", rc);
+}
+
 void pip_checksum_amd_capture(bool on) { t_ctx.capture = on; }
 
 bool pip_checksum_amd_capturing() { return t_ctx.capture; }

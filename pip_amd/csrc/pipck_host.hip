@@ -11,6 +11,8 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
+#include <immintrin.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -30,7 +32,7 @@ static thread_local std::string t_err;
 // (pipck_ctx_zero_copy).
 static int default_zero_copy() {
     const char* e = getenv("PIPCK_HOST_ZERO_COPY");
-    return e && (*e == '0' || *e == '1') ? *e - '0' : 2;
+    return e && *e >= '0' && *e <= '3' ? *e - '0' : 2;
 }
 constexpr size_t kZeroCopyMax = 64u << 10;
 void set_error(const std::string& msg) { t_err = msg; }
@@ -150,6 +152,214 @@ __global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict_
     if (threadIdx.x == 0) __hip_atomic_store(out, nseg ? sum : fold16(sum), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---------------------------------------------------------------------------
+// resident per-packet service (pipck_ctx_zero_copy mode 3)
+// ---------------------------------------------------------------------------
+// A launch per call costs ~10 us (percall_bench), 20x pip's scalar loop on a
+// 1,480-B segment.  In mode 3 one 256-thread block stays resident and polls a
+// doorbell word in coherent pinned host memory: the caller stages the request
+// exactly as the zero-copy path does, writes its parameters, releases a new
+// sequence number and spins on the completion word the block releases after
+// storing the result -- no launch, no stream operation.  The block exits after
+// kResidentIdleMs without a request (or when the context is destroyed), so it
+// never outlives its caller's activity by more than that; the next call
+// relaunches it.  All accesses to the mailbox are system-scope atomics
+// (vector memory); the staged bytes are read after the acquiring load.
+// The request lives in ONE 64-byte line (an x86 cache line, so the device's
+// 64-byte read of it is a consistent snapshot, and the host writes `req`
+// last): a poll is one vector load that returns the sequence number, the
+// parameters and up to kResidentInlineSegs segment (offset, length) pairs, so
+// a request costs two PCIe round trips (the poll, then the bytes) instead of
+// one per dependent field.  Chains of more segments read their SegRef table
+// from the staging buffer.
+constexpr uint32_t kResidentInlineSegs = 5;
+// The doorbell -- host-written, device-polled.  In fine-grained device memory
+// when the host can write that directly (PIPCK_RESIDENT_VRAM=1: large-BAR
+// systems; the device then polls its own HBM), else in coherent pinned host
+// memory (each poll a PCIe read).
+struct alignas(128) ResidentDoorbell {
+    uint32_t req;    // host: sequence number of the posted request (written last)
+    uint32_t nseg, init, pad0;
+    uint64_t bytes;  // device-readable address of the staged segment bytes
+    uint32_t seg[2 * kResidentInlineSegs];  // (offset from `bytes`, length) of the first segments
+    uint32_t pad1[16];
+    alignas(64) uint32_t stop;  // host: end the service
+    uint32_t pad2[15];
+};
+static_assert(offsetof(ResidentDoorbell, pad1) == 64, "the request must fill one 64-byte line");
+// The reply -- device-written, host-polled: always in coherent pinned host memory.
+struct alignas(128) ResidentReply {
+    uint32_t done;  // sequence number of the last completed request (release)
+    uint32_t result;
+    uint32_t alive;  // 1 while the service runs
+    uint32_t pad[29];
+};
+constexpr uint32_t kResidentIdleMs = 50;
+
+__global__ __launch_bounds__(256) void k_resident(const ResidentDoorbell* db, ResidentReply* rp, uint64_t idle_ticks) {
+    __shared__ uint64_t sa[64], sb[64];  // per segment (up to 64 in flight at once), then folded in order
+    __shared__ uint32_t s_line[16];
+    __shared__ uint32_t s_go;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the last request served: the same value in every thread (wave 0 polls against it)
+    uint32_t last = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)__hip_atomic_load(&rp->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (threadIdx.x == 0) __hip_atomic_store(&rp->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* line = reinterpret_cast<const uint32_t*>(db);
+    for (;;) {
+        if (w == 0) {
+            // wave 0 polls: lanes 0..15 read the request line in one 64-byte load
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+            uint32_t go = 0;
+            for (;;) {
+                const uint32_t v = lane < 16 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+                const uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+                if (r != last) {
+                    if (lane < 16) s_line[lane] = v;
+                    go = 1;
+                    break;
+                }
+                if (__hip_atomic_load(&db->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;  // every wave exits
+                __builtin_amdgcn_s_sleep(1);
+            }
+            // the staged bytes were written before `req`: order the reads below after it
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope
+            if (lane == 0) s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) break;
+        const uint32_t req = s_line[0], nseg = s_line[1], init = s_line[2];
+        const uint8_t* bytes = reinterpret_cast<const uint8_t*>((uint64_t)s_line[4] | (uint64_t)s_line[5] << 32);
+        const SegRef* table = reinterpret_cast<const SegRef*>(bytes) - 0;  // SegRef table precedes the bytes
+        uint32_t sum = init;  // thread 0
+        if (nseg <= kResidentInlineSegs) {
+            // every chunk of every segment in one pass over the block: each
+            // thread issues up to 8 loads before summing any, so a request of
+            // up to 32 KiB is one PCIe round trip
+            uint32_t pre[kResidentInlineSegs + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kResidentInlineSegs; k++)
+                pre[k + 1] = pre[k] + (k < nseg ? (s_line[7 + 2 * k] + 15) / 16 : 0u);
+            const uint32_t total = pre[kResidentInlineSegs];
+            uint64_t A[kResidentInlineSegs] = {}, B[kResidentInlineSegs] = {};
+            for (uint32_t c0 = threadIdx.x; c0 < total; c0 += 256 * 8) {
+                u32x4 v[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t c = c0 + 256u * j;
+                    uint32_t k = 0;
+#pragma unroll
+                    for (uint32_t q = 1; q < kResidentInlineSegs; q++) k += c >= pre[q] ? 1u : 0u;
+                    v[j] = c < total ? *reinterpret_cast<const u32x4*>(bytes + s_line[6 + 2 * k] + 16u * (c - pre[k]))
+                                     : u32x4{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t c = c0 + 256u * j;
+                    if (c >= total) continue;
+                    uint32_t k = 0;
+#pragma unroll
+                    for (uint32_t q = 1; q < kResidentInlineSegs; q++) k += c >= pre[q] ? 1u : 0u;
+                    u32x4 x = v[j];
+                    const int hi = (int)s_line[7 + 2 * k] - 16 * (int)(c - pre[k]);
+                    if (hi < 16) x = mask_tail(x, hi);
+                    uint64_t a = 0, b = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {  // offsets 4q+0, 4q+2 even; 4q+1, 4q+3 odd
+                        a += (x[q] & 0xFFu) + ((x[q] >> 16) & 0xFFu);
+                        b += ((x[q] >> 8) & 0xFFu) + (x[q] >> 24);
+                    }
+#pragma unroll
+                    for (uint32_t q = 0; q < kResidentInlineSegs; q++)
+                        if (q == k) {
+                            A[q] += a;
+                            B[q] += b;
+                        }
+                }
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kResidentInlineSegs; q++) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    A[q] += __shfl_xor(A[q], o, 64);
+                    B[q] += __shfl_xor(B[q], o, 64);
+                }
+                if (lane == 0) {
+                    sa[4 * q + w] = A[q];
+                    sb[4 * q + w] = B[q];
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (uint32_t q = 0; q < nseg; q++) {
+                    const uint64_t a = sa[4 * q] + sa[4 * q + 1] + sa[4 * q + 2] + sa[4 * q + 3];
+                    const uint64_t b = sb[4 * q] + sb[4 * q + 1] + sb[4 * q + 2] + sb[4 * q + 3];
+                    sum += (uint32_t)(256ull * a + b);  // pip's u32 wrap, then two folds (pip_checksum.cpp:16-30)
+                    sum = fold16(sum);
+                }
+            __syncthreads();
+        }
+        // longer chains: segments in groups of 64: wave w sums segments w, w+4, ... of the group
+        // (all of one group's loads in flight together), thread 0 then replays
+        // pip's sequential fold over them in order (pip_checksum.cpp:110-112)
+        for (uint32_t g0 = 0; nseg > kResidentInlineSegs && g0 < nseg; g0 += 64) {
+            const uint32_t gn = min(64u, nseg - g0);
+            for (uint32_t k = (uint32_t)w; k < gn; k += 4) {
+                const uint32_t sg = g0 + k;
+                uint32_t off, len;
+                if (sg < kResidentInlineSegs) {
+                    off = s_line[6 + 2 * sg];
+                    len = s_line[7 + 2 * sg];
+                } else {
+                    const SegRef r = *(reinterpret_cast<const SegRef*>(bytes) - (int64_t)(((nseg * sizeof(SegRef) + 15) & ~15ull) / sizeof(SegRef)) + sg);
+                    off = (uint32_t)r.offset;
+                    len = r.len;
+                }
+                const u32x4* base = reinterpret_cast<const u32x4*>(bytes + off);
+                const uint32_t nch = (len + 15) / 16;
+                uint64_t A = 0, B = 0;
+                for (uint32_t c = (uint32_t)lane; c < nch; c += 64) {
+                    u32x4 v = base[c];
+                    const int hi = (int)len - 16 * (int)c;
+                    if (hi < 16) v = mask_tail(v, hi);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {  // offsets 4q+0, 4q+2 even; 4q+1, 4q+3 odd
+                        const uint32_t x = v[q];
+                        A += (x & 0xFFu) + ((x >> 16) & 0xFFu);
+                        B += ((x >> 8) & 0xFFu) + (x >> 24);
+                    }
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    A += __shfl_xor(A, o, 64);
+                    B += __shfl_xor(B, o, 64);
+                }
+                if (lane == 0) {
+                    sa[k] = A;
+                    sb[k] = B;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (uint32_t k = 0; k < gn; k++) {
+                    sum += (uint32_t)(256ull * sa[k] + sb[k]);  // pip's u32 wrap, then two folds
+                    sum = fold16(sum);
+                }
+            __syncthreads();
+        }
+        (void)table;
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(&rp->result, nseg ? sum : fold16(sum), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&rp->done, req, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        last = req;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(&rp->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace pipck
 
 using namespace pipck;
@@ -172,6 +382,13 @@ struct pipck_ctx {
     void* d_flows = nullptr;
     uint32_t flows_cap = 0;
     int zero_copy = 2;  // pipck_host_sum path (pipck_ctx_zero_copy)
+    // resident service (mode 3): its own stream, a mailbox in coherent pinned memory
+    hipStream_t res_stream = nullptr;
+    ResidentDoorbell* db = nullptr;
+    bool db_vram = false;
+    ResidentReply* rp = nullptr;
+    uint32_t res_seq = 0;
+    bool res_launched = false;
     std::mutex mu;
 };
 
@@ -188,8 +405,61 @@ struct DeviceGuard {
     }
 };
 
+// Mode 3: make sure the resident block runs (launching it if it never ran or
+// has exited after its idle timeout).
+int resident_start(pipck_ctx* c) {
+    if (!c->rp) {
+        const char* e = getenv("PIPCK_RESIDENT_VRAM");
+        c->db_vram = e && *e == '1' &&
+                     hipExtMallocWithFlags((void**)&c->db, sizeof(ResidentDoorbell), hipDeviceMallocFinegrained) == hipSuccess;
+        if (!c->db_vram) PIPCK_HIP(hipHostMalloc((void**)&c->db, sizeof(ResidentDoorbell), hipHostMallocCoherent));
+        for (size_t i = 0; i < sizeof(ResidentDoorbell) / 4; i++) ((volatile uint32_t*)c->db)[i] = 0;
+        PIPCK_HIP(hipHostMalloc((void**)&c->rp, sizeof(ResidentReply), hipHostMallocCoherent));
+        std::memset((void*)c->rp, 0, sizeof(ResidentReply));
+        PIPCK_HIP(hipStreamCreateWithFlags(&c->res_stream, hipStreamNonBlocking));
+        c->res_seq = 0;
+    }
+    if (c->res_launched) {
+        if (__atomic_load_n(&c->rp->alive, __ATOMIC_ACQUIRE)) return PIPCK_OK;
+        const hipError_t q = hipStreamQuery(c->res_stream);
+        if (q == hipErrorNotReady) return PIPCK_OK;  // launched, not started yet
+        if (q != hipSuccess) PIPCK_HIP(q);
+    }
+    ((volatile uint32_t*)&c->db->stop)[0] = 0u;
+    _mm_sfence();
+    // the service may have finished requests up to res_seq; it resumes from `done`
+    hipLaunchKernelGGL(k_resident, dim3(1), dim3(256), 0, c->res_stream, c->db, c->rp,
+                       (uint64_t)kResidentIdleMs * 100000ull);
+    PIPCK_LAUNCHED("k_resident");
+    c->res_launched = true;
+    return PIPCK_OK;
+}
+
+void resident_halt(pipck_ctx* c) {  // end the block (it restarts on the next call)
+    if (!c->res_launched) return;
+    ((volatile uint32_t*)&c->db->stop)[0] = 1u;
+    _mm_sfence();
+    (void)hipStreamSynchronize(c->res_stream);  // the block sees stop within one poll
+    c->res_launched = false;
+}
+
+void resident_stop(pipck_ctx* c) {
+    if (!c->rp) return;
+    resident_halt(c);
+    if (c->res_stream) (void)hipStreamDestroy(c->res_stream);
+    if (c->db_vram) (void)hipFree(c->db);
+    else (void)hipHostFree(c->db);
+    (void)hipHostFree(c->rp);
+    c->db = nullptr;
+    c->rp = nullptr;
+    c->res_stream = nullptr;
+}
+
 int grow_stage(pipck_ctx* c, size_t need) {
     if (need <= c->stage_cap) return PIPCK_OK;
+    // hipHostFree / hipFree wait for the device: end the resident block first
+    // (it restarts on its own on the next call)
+    resident_halt(c);
     size_t cap = need < (1u << 20) ? (1u << 20) : need + need / 2;
     if (c->h_stage) PIPCK_HIP(hipHostFree(c->h_stage));
     if (c->d_stage) PIPCK_HIP(hipFree(c->d_stage));
@@ -247,6 +517,7 @@ int pipck_ctx_create(int device, pipck_ctx** out) {
 int pipck_ctx_destroy(pipck_ctx* c) {
     if (!c) return PIPCK_OK;
     DeviceGuard g(c->device);
+    resident_stop(c);
     for (int i = 0; i < 2; i++) {
         if (c->stream[i]) (void)hipStreamSynchronize(c->stream[i]);
         if (c->d_chunk[i]) (void)hipFree(c->d_chunk[i]);
@@ -292,7 +563,45 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
     }
     hipStream_t s = c->stream[0];
     const int zc = c->zero_copy;
-    if (zc == 1 || (zc == 2 && need <= kZeroCopyMax)) {
+    if (zc == 3 && need <= kZeroCopyMax) {
+        // the resident block: post the request, spin on its completion word
+        if ((rc = resident_start(c))) return rc;
+        ResidentDoorbell* db = c->db;
+        ResidentReply* rp = c->rp;
+        const uint32_t seq = ++c->res_seq;
+        volatile uint32_t* line = reinterpret_cast<volatile uint32_t*>(db);
+        line[1] = nseg;
+        line[2] = init;
+        const uint64_t bytes = (uint64_t)(uintptr_t)(c->h_stage + table);
+        line[4] = (uint32_t)bytes;
+        line[5] = (uint32_t)(bytes >> 32);
+        for (uint32_t i = 0; i < nseg && i < kResidentInlineSegs; i++) {
+            line[6 + 2 * i] = (uint32_t)refs[i].offset;
+            line[7 + 2 * i] = refs[i].len;
+        }
+        // the staged bytes and the parameters before the sequence number (the
+        // doorbell may be write-combined device memory)
+        _mm_sfence();
+        line[0] = seq;
+        _mm_sfence();
+        auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(&rp->done, __ATOMIC_ACQUIRE) != seq) {
+            const auto el = std::chrono::steady_clock::now() - t0;
+            if (el > std::chrono::milliseconds(2)) {
+                // the block may have hit its idle timeout just before the post:
+                // relaunch it (it resumes from `done`, so it serves this request)
+                if ((rc = resident_start(c))) return rc;
+                if (el > std::chrono::seconds(2)) {
+                    set_error("pipck_host_sum: the resident service did not answer within 2 s");
+                    return PIPCK_EHIP;
+                }
+            }
+            __builtin_ia32_pause();
+        }
+        *out = __atomic_load_n(&rp->result, __ATOMIC_RELAXED);
+        return PIPCK_OK;
+    }
+    if (zc == 1 || (zc >= 2 && need <= kZeroCopyMax)) {
         // The kernel reads the pinned staging buffer over PCIe and writes the
         // result into pinned host memory: no copy commands around the launch.
         // The result (<= 0xFFFF) replaces a sentinel no sum can take; the host
@@ -327,11 +636,13 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
 }
 
 int pipck_ctx_zero_copy(pipck_ctx* c, int mode) {
-    if (!c || mode < 0 || mode > 2) {
-        set_error("pipck_ctx_zero_copy: null context or mode outside 0..2");
+    if (!c || mode < 0 || mode > 3) {
+        set_error("pipck_ctx_zero_copy: null context or mode outside 0..3");
         return PIPCK_EINVAL;
     }
     std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    if (mode != 3) resident_stop(c);  // release the resident block's CU slot
     c->zero_copy = mode;
     return PIPCK_OK;
 }

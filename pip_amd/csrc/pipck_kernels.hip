@@ -223,7 +223,9 @@ constexpr uint32_t kNoPackedTiles = 16u;  // pipck_tune flags bit 4: ragged tile
 constexpr uint32_t kWideBlocks = 32u;     // pipck_tune flags bit 5: 4-wave ragged blocks instead of 1-wave
 template <uint32_t WPB = 4>  // waves per block
 __device__ __forceinline__ TaskRange xcd_tasks(uint64_t n_tasks, bool grouped) {
-    const uint32_t w = threadIdx.x >> 6;
+    // wave-uniform as far as the compiler knows too: task addresses feed scalar
+    // buffer resources, and a "divergent" one is wrapped in a readfirstlane loop
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (!grouped || gridDim.x < 8) return {(uint64_t)blockIdx.x * WPB + w, n_tasks, (uint64_t)gridDim.x * WPB};
     const uint32_t g = blockIdx.x & 7, gi = blockIdx.x >> 3;
     const uint32_t nb = (gridDim.x - g + 7) >> 3;  // blocks in group g

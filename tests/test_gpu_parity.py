@@ -94,6 +94,31 @@ def test_every_known_answer_on_gpu_zero_copy(kat):
         pc.set_zero_copy(2)
 
 
+def test_every_known_answer_on_gpu_resident(kat):
+    """The same known answers through the resident service (mode 3: one block
+    stays on the GPU polling a doorbell; requests over 64 KiB -- the 131,076-B
+    wrap KATs -- take the zero-copy launch).  The block's idle exit and
+    relaunch are exercised too: a pause longer than its 50 ms idle timeout,
+    then more calls."""
+    import time
+
+    pc.set_zero_copy(3)
+    try:
+        bad = [c["fn"] for c in kat if run_case(PcAdapter, c) != c["expect"]]
+        assert not bad, bad[:5]
+        time.sleep(0.12)  # the block has exited by now
+        small = [c for c in kat if c["fn"] != "fold"][:40]
+        bad = [c["fn"] for c in small if run_case(PcAdapter, c) != c["expect"]]
+        assert not bad, bad[:5]
+        # switching modes ends the block; switching back restarts it
+        pc.set_zero_copy(1)
+        pc.set_zero_copy(3)
+        bad = [c["fn"] for c in small if run_case(PcAdapter, c) != c["expect"]]
+        assert not bad, bad[:5]
+    finally:
+        pc.set_zero_copy(2)
+
+
 def test_per_packet_api_is_thread_safe(kat):
     cases = [c for c in kat if c["fn"] != "fold"][:60]
     errors = []

@@ -57,7 +57,8 @@ def worker(only: list[str], iters: int) -> None:
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
         ms = statistics.median(timed(run, iters) for _ in range(3))
         digest = hashlib.sha256(run().cpu().numpy().tobytes()).hexdigest()[:16]
-        print(json.dumps({"workload": w.name + ("+pseudo" if fam and not w.family else ""), "packets": n, "ms": ms,
+        tag = ("+pseudo" if fam and not w.family else "") + ("+desc" if name == "cfg4d" else "")
+        print(json.dumps({"workload": w.name + tag, "packets": n, "ms": ms,
                           "bytes": nbytes, "sha": digest}), flush=True)
         del arena
         torch.cuda.empty_cache()
