@@ -22,6 +22,13 @@
 //   _ref/stack_tx_zero: every checksum returns 0 (oracle/ck_zero.cpp)    --mode zero
 //        pip's TX path with no checksum work: the ceiling of any offload (wrong wire bytes)
 //
+// --conns K opens K connections (client ports 40000+k) and writes to them in
+// turn.  --pipeline (capture modes, K >= 2) overlaps the GPU with pip: after
+// each write pip_checksum_amd_submit() starts that write's batch and completes
+// the previous one, whose packets are then output and its connection ACKed
+// while the GPU works on the next (pip waits for the ACK of a write's PUSH
+// before that connection's next write, so overlap needs another connection).
+//
 // Output (one JSON line): payload GiB/s and packets/s through the whole TX path, and a
 // digest of every emitted packet -- with --verify, FNV-1a over every wire byte; else over
 // each packet's IPv4 and TCP checksum fields and length -- which must be equal across the
@@ -52,11 +59,19 @@ enum Mode { REF, SYNC, CAPTURE, CAPTURE_ZC, ZERO };
 Mode g_mode = REF;
 bool g_verify = false;
 bool g_hold = false;  // capture modes: packets wait for the flush
-std::shared_ptr<pip_tcp> g_tcp;
+struct Conn {
+    uint16_t port;
+    std::shared_ptr<pip_tcp> tcp;
+    uint32_t cseq = 7000;
+    uint32_t srv_next = 0;  // pip's next sequence number on this connection, from its emitted segments
+    uint8_t* buf = nullptr;
+};
+std::vector<Conn> g_conns;
+int g_connecting = -1;  // the connection whose SYN is being input
+constexpr uint16_t kPortBase = 40000;
 std::vector<std::vector<std::shared_ptr<pip_buf>>> g_pending;
 uint64_t g_digest = 1469598103934665603ull;
 uint64_t g_packets = 0, g_wire_bytes = 0;
-uint32_t g_srv_next = 0;  // pip's next sequence number, from the emitted segments
 FILE* g_dump = nullptr;   // --dump: one 12-byte record per packet (seq, ip_id, ip_sum, th_sum, length)
 
 inline void fnv(const uint8_t* p, size_t n) {
@@ -84,9 +99,10 @@ void emit(const std::vector<std::shared_ptr<pip_buf>>& segs) {
     if (segs.size() > 1 && segs[1]->payload_len() >= 8) {
         const uint8_t* th = (const uint8_t*)segs[1]->payload();
         const uint32_t seq = (uint32_t)th[4] << 24 | (uint32_t)th[5] << 16 | (uint32_t)th[6] << 8 | th[7];
+        const unsigned k = (unsigned)(th[2] << 8 | th[3]) - kPortBase;  // pip's destination = the client port
         size_t data = 0;
         for (size_t i = 2; i < segs.size(); i++) data += segs[i]->payload_len();
-        g_srv_next = seq + (uint32_t)data + ((th[13] & (TH_SYN | TH_FIN)) ? 1 : 0);
+        if (k < g_conns.size()) g_conns[k].srv_next = seq + (uint32_t)data + ((th[13] & (TH_SYN | TH_FIN)) ? 1 : 0);
     }
     if (g_dump) {
         const uint8_t* ip = (const uint8_t*)segs[0]->payload();
@@ -111,6 +127,13 @@ void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
     // it did is reported as invalid rather than digested
     if (std::this_thread::get_id() != g_main) {
         g_retransmits++;
+        auto q = buf->next();  // the TCP header segment: which packet pip resent
+        if (q && q->payload_len() >= 14) {
+            const uint8_t* th = (const uint8_t*)q->payload();
+            fprintf(stderr, "retransmit: port %u seq %u flags 0x%02x at %.3f s\n", (unsigned)(th[2] << 8 | th[3]),
+                    (uint32_t)th[4] << 24 | (uint32_t)th[5] << 16 | (uint32_t)th[6] << 8 | th[7], th[13],
+                    std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+        }
         return;
     }
     std::vector<std::shared_ptr<pip_buf>> segs;
@@ -132,15 +155,15 @@ void settle() {
 }
 
 void on_connect(pip_netif&, std::shared_ptr<pip_tcp> tcp, const void* hs, pip_uint16) {
-    g_tcp = tcp;
+    if (g_connecting >= 0) g_conns[g_connecting].tcp = tcp;
     tcp->connected(hs);
 }
 
 void put16(uint8_t* p, uint16_t v) { p[0] = v >> 8; p[1] = (uint8_t)v; }
 void put32(uint8_t* p, uint32_t v) { put16(p, v >> 16); put16(p + 2, (uint16_t)v); }
 
-// a client segment to pip (10.0.0.2:40000 -> 10.0.0.1:80); RX takes no checksum
-std::vector<uint8_t> craft(uint32_t seq, uint32_t ack, uint8_t flags, const std::vector<uint8_t>& opts) {
+// a client segment to pip (10.0.0.2:port -> 10.0.0.1:80); RX takes no checksum
+std::vector<uint8_t> craft(uint16_t port, uint32_t seq, uint32_t ack, uint8_t flags, const std::vector<uint8_t>& opts) {
     const size_t thl = 20 + opts.size();
     std::vector<uint8_t> p(20 + thl, 0);
     p[0] = 0x45;
@@ -151,7 +174,7 @@ std::vector<uint8_t> craft(uint32_t seq, uint32_t ack, uint8_t flags, const std:
     memcpy(&p[12], cli, 4);
     memcpy(&p[16], srv, 4);
     uint8_t* t = &p[20];
-    put16(t, 40000);
+    put16(t, port);
     put16(t + 2, 80);
     put32(t + 4, seq);
     put32(t + 8, ack);
@@ -172,6 +195,8 @@ int main(int argc, char** argv) {
     std::string mode = "ref";
     unsigned mss = 1460;
     size_t total = 256ull << 20, per_write = 4ull << 20;
+    unsigned conns = 1;
+    bool pipeline = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto val = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
@@ -180,6 +205,8 @@ int main(int argc, char** argv) {
         else if (a == "--bytes") total = strtoull(val(), nullptr, 0);
         else if (a == "--write") per_write = strtoull(val(), nullptr, 0);
         else if (a == "--verify") g_verify = true;
+        else if (a == "--conns") conns = (unsigned)atoi(val());
+        else if (a == "--pipeline") pipeline = true;
         else if (a == "--dump") g_dump = fopen(val(), "wb");
         else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }
@@ -196,22 +223,33 @@ int main(int argc, char** argv) {
 #else
     if (g_mode == REF) { fprintf(stderr, "this build links libpip_checksum_amd.so: sync/capture/capture_zc\n"); return 2; }
 #endif
-    if (mss < 1 || mss > 65495 || per_write < 1 || per_write > (1u << 30)) {
-        fprintf(stderr, "bad --mss / --write\n");
+    if (mss < 1 || mss > 65495 || per_write < 1 || per_write > (1u << 30) || conns < 1 || conns > 64) {
+        fprintf(stderr, "bad --mss / --write / --conns\n");
+        return 2;
+    }
+    if (pipeline && (conns < 2 || (g_mode != CAPTURE && g_mode != CAPTURE_ZC))) {
+        fprintf(stderr, "--pipeline needs a capture mode and --conns >= 2\n");
         return 2;
     }
 
-    // the application's send buffer: pip's pip_buf points into it (write(..., is_copy=false))
-    uint8_t* buf = nullptr;
+    // each connection's send buffer: pip's pip_buf points into it (write(..., is_copy=false));
+    // a buffer is rewritten only after its connection's previous write was ACKed
+    g_conns.resize(conns);
+    std::vector<std::vector<uint8_t>> plain(conns);
+    for (unsigned k = 0; k < conns; k++) {
+        g_conns[k].port = (uint16_t)(kPortBase + k);
+        uint8_t* b = nullptr;
 #ifdef PIPCK_AMD
-    if (g_mode == CAPTURE_ZC) buf = (uint8_t*)pipck_host_alloc(per_write);
+        if (g_mode == CAPTURE_ZC) b = (uint8_t*)pipck_host_alloc(per_write);
 #endif
-    std::vector<uint8_t> plain;
-    if (!buf) {
-        plain.resize(per_write);
-        buf = plain.data();
+        if (!b) {
+            plain[k].resize(per_write);
+            b = plain[k].data();
+        }
+        for (size_t i = 0; i < per_write; i++) b[i] = (uint8_t)(i * 131 + (i >> 11) * 7 + 1 + k);
+        g_conns[k].buf = b;
     }
-    for (size_t i = 0; i < per_write; i++) buf[i] = (uint8_t)(i * 131 + (i >> 11) * 7 + 1);
+    uint8_t* buf = g_conns[0].buf;
 
     g_main = std::this_thread::get_id();
     // One-time GPU initialisation (device, streams, every kernel the calls below
@@ -247,32 +285,64 @@ int main(int argc, char** argv) {
     nif.output_ip_data_callback = on_output;
     nif.new_tcp_connect_callback = on_connect;
 
-    uint32_t cseq = 7000;
     const std::vector<uint8_t> opts = {2, 4, (uint8_t)(mss >> 8), (uint8_t)mss, 3, 3, 14, 1};
-    auto syn = craft(cseq, 0, TH_SYN, opts);
-    nif.input(syn.data());
-    settle();
-    if (!g_tcp) { fprintf(stderr, "no connection\n"); return 1; }
-    cseq += 1;
-    auto ack = craft(cseq, g_srv_next, TH_ACK, {});
-    nif.input(ack.data());
-    settle();
+    for (unsigned k = 0; k < conns; k++) {
+        Conn& c = g_conns[k];
+        g_connecting = (int)k;
+        auto syn = craft(c.port, c.cseq, 0, TH_SYN, opts);
+        nif.input(syn.data());
+        settle();
+        if (!c.tcp) { fprintf(stderr, "no connection %u\n", k); return 1; }
+        c.cseq += 1;
+        auto ack = craft(c.port, c.cseq, c.srv_next, TH_ACK, {});
+        nif.input(ack.data());
+        settle();
+    }
+    g_connecting = -1;
+    auto ack_conn = [&](unsigned k) {  // the peer ACKs everything pip sent on connection k (and its PUSH)
+        auto a = craft(g_conns[k].port, g_conns[k].cseq, g_conns[k].srv_next, TH_ACK, {});
+        nif.input(a.data());
+    };
 
     const uint64_t pk0 = g_packets;
     size_t sent = 0;
     unsigned writes = 0;
+    int prev = -1;  // --pipeline: the connection whose batch is in flight
+    std::vector<std::vector<std::shared_ptr<pip_buf>>> inflight;
     const double t0 = now();
+    fprintf(stderr, "timed region starts at %.3f s\n", t0);
     while (sent < total) {
+        const unsigned k = writes % conns;
         const size_t want = total - sent < per_write ? total - sent : per_write;
-        const uint32_t w = g_tcp->write(buf, (pip_uint32)want, false);
-        settle();
+        const uint32_t w = g_conns[k].tcp->write(g_conns[k].buf, (pip_uint32)want, false);
         if (w == 0) { fprintf(stderr, "write stalled at %zu bytes\n", sent); return 1; }
         sent += w;
         writes++;
-        auto a = craft(cseq, g_srv_next, TH_ACK, {});  // the peer ACKs the whole write (and its PUSH)
-        nif.input(a.data());
+#ifdef PIPCK_AMD
+        if (pipeline) {
+            // start this write's batch; the previous one completes (fields stored)
+            pip_checksum_amd_submit();
+            for (auto& sg : inflight) emit(sg);
+            inflight.clear();
+            if (prev >= 0) ack_conn((unsigned)prev);
+            inflight.swap(g_pending);  // this write's packets (and anything the ACK produced) wait for the next submit
+            prev = (int)k;
+            continue;
+        }
+#endif
+        settle();
+        ack_conn(k);
         settle();
     }
+#ifdef PIPCK_AMD
+    if (pipeline) {
+        pip_checksum_amd_complete();
+        for (auto& sg : inflight) emit(sg);
+        inflight.clear();
+        if (prev >= 0) ack_conn((unsigned)prev);
+        settle();
+    }
+#endif
     const double el = now() - t0;
     const uint64_t pk = g_packets - pk0;
 #ifdef PIPCK_AMD
@@ -282,10 +352,10 @@ int main(int argc, char** argv) {
     }
 #endif
     printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
-           "\"writes\": %u, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
+           "\"writes\": %u, \"conns\": %u, \"pipeline\": %s, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
            "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu, "
            "\"cold_ms\": {\"first_calls\": %.3f, \"first_flush\": %.3f, \"second_flush\": %.3f}}\n",
-           mode.c_str(), mss, per_write, sent, writes, (unsigned long long)pk, el, sent / el / (1u << 30),
+           mode.c_str(), mss, per_write, sent, writes, conns, pipeline ? "true" : "false", (unsigned long long)pk, el, sent / el / (1u << 30),
            pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
            (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load(), cold[0] * 1e3, cold[1] * 1e3,
            cold[2] * 1e3);
