@@ -57,3 +57,36 @@ def test_pip_stack_on_amd_checksum_is_byte_identical(capture):
     zc = lines[-1].split()
     assert zc[zc.index("free_while_queued") + 1] == "6"  # PIPCK_EBUSY
     assert zc[zc.index("free_after") + 1] == "0"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mss", [1460, 8960])
+def test_pip_tx_path_at_volume_matches_pip(mss):
+    """pip's TCP write() path at volume (oracle/stack_tx_bench.cpp): pip's own
+    build vs the drop-in synchronously, in capture mode, with zero-copy, and
+    pipelined across two connections -- FNV-1a over every emitted wire byte must
+    be identical, and pip's retransmit timer must never fire."""
+    import json
+    import os
+
+    ref_bin = ROOT / "oracle" / "_ref" / "stack_tx_ref"
+    amd_bin = ROOT / "oracle" / "_ref" / "stack_tx_amd"
+    assert ref_bin.exists() and amd_bin.exists(), "build with `make -C oracle ref ref-amd`"
+
+    def run(binary, *args):
+        r = subprocess.run([str(binary), "--mss", str(mss), "--bytes", str(8 << 20), "--write", str(1 << 20),
+                            "--verify", *args], capture_output=True, text=True, timeout=120, env=dict(os.environ))
+        assert r.returncode == 0, (args, r.stderr[-2000:])
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["retransmits"] == 0 and d["digest_of"] == "every wire byte"
+        return d["digest"], d["packets"]
+
+    for conns in ("1", "2"):
+        want = run(ref_bin, "--conns", conns)
+        modes = [("--mode", "capture"), ("--mode", "capture_zc")]
+        if conns == "1":
+            modes.append(("--mode", "sync"))
+        else:
+            modes.append(("--mode", "capture_zc", "--pipeline"))
+        for m in modes:
+            assert run(amd_bin, "--conns", conns, *m) == want, (conns, m)
