@@ -285,80 +285,6 @@ __device__ __forceinline__ void trace_task(uint32_t kflags, const TraceBuf& tb, 
 }
 
 // ---------------------------------------------------------------------------
-// persistent wave tasks from per-XCD queue heads (work stealing at the end)
-// ---------------------------------------------------------------------------
-// The task timeline (tools/task_trace.py, profiles/r02_task_trace*.jsonl)
-// showed the dispatcher's static deal (block i to XCD i % 8) finishing the
-// eight XCDs up to 35-120 us apart: their HBM rates differ by ~5 %, and every
-// XCD must work through an eighth of the tasks.  Here a resident grid of
-// waves claims tasks instead.  XCD x owns tasks x, x+8, x+16, ... through its
-// own head word (one word serves ~88 dequeues/us, MI355X_MICROARCH.md
-// 'dequeue'; eight heads keep the claims off one line), so the tasks in flight
-// still sweep the arena as one window; a wave whose XCD has run out steals
-// from the other heads, so the XCDs finish together.  The claim for a wave's
-// next task is issued when its current task starts and read when it ends (a
-// returning atomic ahead of the row loads), so a claim costs no wait.
-// Correctness never depends on placement: every task index below n_tasks is
-// handed out exactly once, whatever XCC_ID reads.  The last wave to leave
-// resets the heads (device-scope atomics), so the queue is ready for the next
-// launch on its stream (launch_queue() keeps one queue per stream).
-constexpr uint32_t kQueueStride = 32;  // u32 words between heads (128 B)
-constexpr uint64_t kNoTask = ~0ull;
-
-struct QueueTasks {
-    uint32_t* q;
-    uint64_t n_tasks;
-    uint32_t x;       // this wave's XCD (0..7)
-    bool own;         // own head not yet exhausted
-    uint32_t pend;    // lane 0: the prefetched claim on the own head
-    int lane;
-
-    __device__ __forceinline__ uint32_t claim(uint32_t h) {  // wave-uniform result
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(&q[h * kQueueStride], 1u);
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-    }
-    __device__ __forceinline__ uint64_t steal() {
-        for (uint32_t k = 1; k < 8; k++) {
-            const uint32_t y = (x + k) & 7u;
-            const uint64_t t = (uint64_t)claim(y) * 8u + y;
-            if (t < n_tasks) return t;
-        }
-        return kNoTask;
-    }
-    __device__ __forceinline__ uint64_t first() {
-        const uint64_t t = (uint64_t)claim(x) * 8u + x;
-        if (t < n_tasks) return t;
-        own = false;
-        return steal();
-    }
-    // at a task's start: the own-head claim for the wave's next task
-    __device__ __forceinline__ void prefetch() {
-        if (own && lane == 0) pend = atomicAdd(&q[x * kQueueStride], 1u);
-    }
-    __device__ __forceinline__ uint64_t next() {
-        if (own) {
-            const uint64_t t = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)pend) * 8u + x;
-            if (t < n_tasks) return t;
-            own = false;
-        }
-        return steal();
-    }
-    // every wave of the grid calls this once, after its last task
-    __device__ __forceinline__ void leave(uint32_t n_waves) {
-        if (lane != 0) return;
-        if (atomicAdd(&q[8 * kQueueStride], 1u) == n_waves - 1) {
-            for (uint32_t h = 0; h <= 8; h++) atomicExch(&q[h * kQueueStride], 0u);
-        }
-    }
-};
-
-__device__ __forceinline__ QueueTasks queue_tasks(uint32_t* q, uint64_t n_tasks, int lane) {
-    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
-    return QueueTasks{q, n_tasks, xcc & 7u, true, 0u, lane};
-}
-
-// ---------------------------------------------------------------------------
 // flat-stream kernel: fixed strides of whole 16-byte chunks, >= 64 chunks each
 // ---------------------------------------------------------------------------
 // A wave owns a run of consecutive packets and streams their chunks as
@@ -600,111 +526,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
         trace_task(kflags, trb, task, t_start, lane);
         wave_sync();
     }
-}
-
-// ---------------------------------------------------------------------------
-// persistent flat-stream kernel: one continuous ring across queue-claimed tasks
-// ---------------------------------------------------------------------------
-// The k_flat stream, but each wave lives for the whole launch (a resident grid)
-// and claims its tasks from the per-XCD queue heads (QueueTasks), so the XCDs
-// finish together, and the ring never drains between tasks: every task spans
-// exactly m*U rows (its packets fill <= m*U rows; rows past its end read zeros
-// from the range-checked buffer, no memory request), so the reloads of a
-// task's last batch are the NEXT task's first U rows, slot for slot.  The one
-// full wait per task comes after those reloads: the claim of the task after
-// next and this task's pseudo-header bases are read together (vmcnt(0)),
-// while the next task's rows are already in flight, then the results are
-// stored.  Needs stride == 16 * ceil(len / 16) (no whole padding chunks: cfg2,
-// cfg3, cfg5); launch_fixed falls back to k_flat otherwise.
-template <int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_cont(
-    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run, uint32_t m,
-    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ queue) {
-    extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16
-    const int lane = threadIdx.x & 63;
-    const uint32_t pitch = flat_pitch(run);
-    uint16_t* part = s_part + (threadIdx.x >> 6) * 64u * pitch;
-    const uint32_t nch = cpp;                                    // launch_fixed: no whole padding chunks
-    const int tail = (int)len - 16 * ((int)nch - 1);             // valid bytes of the last data chunk
-    const uint32_t lterm = len_term(len);
-    const uint64_t n_tasks = (n + run - 1) / run;
-    const uint32_t rows_per_task = m * (uint32_t)U;
-    const TraceBuf trb = trace_buf(kflags);
-    QueueTasks qt = queue_tasks(queue, n_tasks, lane);
-    // tune flags bit 23: a static grid-stride deal instead of the queue (for A/B only)
-    const bool stat = (kflags & (1u << 23)) != 0;
-    const uint64_t gw = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 4u;
-    uint64_t sk = 0;
-    auto claim_static = [&]() -> uint64_t {
-        const uint64_t t = gw + nw * sk++;
-        return t < n_tasks ? t : kNoTask;
-    };
-    const u32x4* a16 = reinterpret_cast<const u32x4*>(arena);
-    auto task_buf = [&](uint64_t t) -> buf_t {  // a task's chunks; no task: an empty buffer (zeros, no requests)
-        if (t == kNoTask) return buf_rsrc(arena, 0u);
-        const uint64_t p0 = t * run;
-        return buf_rsrc(a16 + p0 * cpp, (uint32_t)min<uint64_t>((uint64_t)run, n - p0) * cpp * 16u);
-    };
-    uint64_t task = stat ? claim_static() : qt.first();
-    uint64_t next = task != kNoTask ? (stat ? claim_static() : qt.first()) : kNoTask;  // own head again (or a steal)
-    u32x4 v[U];
-    {
-        const buf_t tb = task_buf(task);
-#pragma unroll
-        for (int u = 0; u < U; u++) v[u] = buf_load<NT>(tb, (uint32_t)(u * 64 + lane) * 16u);
-    }
-    // one loop over ring batches, the task switching inside it (a nested
-    // batch loop made the compiler's wait analysis fall back to vmcnt(0) per row)
-    uint64_t t_start = (kflags & kTrace) ? trace_clock() : 0;
-    uint64_t p0 = task * run;
-    uint32_t np = task != kNoTask ? (uint32_t)min<uint64_t>((uint64_t)run, n - p0) : 0u;
-    uint32_t tchunks = np * cpp;
-    buf_t tb = task_buf(task), tbn = task_buf(next);
-    uint64_t acc = 0;
-    RowPos pp{0, 0};
-    uint32_t b = 0;
-    while (task != kNoTask) {
-        const bool last = b + 1 == m;  // wave-uniform: this batch's reloads are the next task's first rows
-        const buf_t rb = last ? tbn : tb;
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t rs = b * 64u * U + u * 64u;
-            if (rs < tchunks)
-                flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
-            else  // a row past the task (zeros): still consume the slot, so the reload into it
-                asm volatile("" ::"v"(v[u]));  // waits for this row alone, not for every load (vmcnt(0))
-            pp.advance(cpp);
-            const uint32_t r = last ? (uint32_t)(u * 64) : rs + 64u * U;
-            v[u] = buf_load<NT>(rb, (r + lane) * 16u);
-        }
-        if (++b < m) continue;
-        // task done: the one full wait per task -- the claim of the task after
-        // next and this task's pseudo-header bases, read while the next task's
-        // first rows are in flight -- then the results
-        flat_stash(acc, np - 1, part, pitch, lane);
-        if (next != kNoTask && !stat) qt.prefetch();
-        const uint32_t fo = flat_flow_of(p0, np, pseudo, flow_of, lane);
-        const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, fo, flow_origin, lane);
-        const uint64_t after = next != kNoTask ? (stat ? claim_static() : qt.next()) : kNoTask;
-        wave_sync();
-        flat_write<VERIFY>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane);
-        trace_task(kflags, trb, task, t_start, lane);
-        wave_sync();
-        task = next;
-        next = after;
-        t_start = (kflags & kTrace) ? trace_clock() : 0;
-        p0 = task * run;
-        np = task != kNoTask ? (uint32_t)min<uint64_t>((uint64_t)run, n - p0) : 0u;
-        tchunks = np * cpp;
-        tb = tbn;
-        tbn = task_buf(next);
-        acc = 0;
-        pp = RowPos{0, 0};
-        b = 0;
-        (void)rows_per_task;
-    }
-    qt.leave(gridDim.x * 4u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1523,43 +1344,6 @@ static const FlatVariant kFlat[] = {PIPCK_F(2, false), PIPCK_F(4, false), PIPCK_
                                     PIPCK_F(2, true),  PIPCK_F(4, true),  PIPCK_F(8, true),  PIPCK_F(12, true),
                                     PIPCK_F(16, true), PIPCK_F(32, true), PIPCK_F(24, true)};
 #undef PIPCK_F
-// one-wave blocks (tune flags bit 21): a finished wave's slot is refilled at once
-// instead of waiting for its block's three other waves
-constexpr uint32_t kFlatOneWave = 1u << 21;
-#define PIPCK_F1(U) \
-    { {k_flat<U, true, false, false, 1>, k_flat<U, true, false, true, 1>}, {k_flat<U, true, true, false, 1>, k_flat<U, true, true, true, 1>} }
-static const flat_fn kFlat1[3][2][2] = {PIPCK_F1(16), PIPCK_F1(24), PIPCK_F1(32)};  // [ring 16/24/32][verify][nt]
-#undef PIPCK_F1
-// the persistent continuous-ring kernel (k_flat_cont), tune flags bit 22
-constexpr uint32_t kFlatQueue = 1u << 22;
-typedef void (*flatc_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, uint32_t, const uint32_t*, uint32_t,
-                         const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t, uint32_t*);
-#define PIPCK_FC(U) \
-    { {k_flat_cont<U, false, false>, k_flat_cont<U, false, true>}, {k_flat_cont<U, true, false>, k_flat_cont<U, true, true>} }
-static const flatc_fn kFlatCont[3][2][2] = {PIPCK_FC(16), PIPCK_FC(24), PIPCK_FC(32)};  // [ring 16/24/32][verify][nt]
-#undef PIPCK_FC
-
-// One task queue (8 heads + a leave counter, zeroed) per (device, stream):
-// kernels on one stream run one after another, and each launch leaves its
-// queue zeroed, so a stream's launches can share one.
-static uint32_t* launch_queue(hipStream_t s) {
-    static std::mutex mu;
-    static std::vector<std::pair<std::pair<int, hipStream_t>, uint32_t*>> qs;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    for (auto& e : qs)
-        if (e.first.first == dev && e.first.second == s) return e.second;
-    uint32_t* q = nullptr;
-    const size_t bytes = 9 * kQueueStride * sizeof(uint32_t);
-    if (hipMalloc((void**)&q, bytes) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(q, 0, bytes, s) != hipSuccess) {
-        (void)hipFree(q);
-        return nullptr;
-    }
-    qs.push_back({{dev, s}, q});
-    return q;
-}
 static const flat_fn kFlatSmall[2][2] = {  // [verify][nt]
     {k_flat_small<16, false, false>, k_flat_small<16, false, true>},
     {k_flat_small<16, true, false>, k_flat_small<16, true, true>}};
@@ -1647,40 +1431,8 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 128u : 64u);
         const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
-        const int r1 = fv->pipe ? (fv->u == 16 ? 0 : fv->u == 24 ? 1 : fv->u == 32 ? 2 : -1) : -1;
-        if ((flags & kFlatOneWave) && r1 >= 0) {
-            const size_t lds1 = 64u * flat_pitch(run) * sizeof(uint16_t);
-            hipLaunchKernelGGL(kFlat1[r1][verify][nt_for(true)], dim3(grid_for(1, tasks, 0)), dim3(64), lds1,
-                               as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
-                               n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
-            PIPCK_LAUNCHED("k_flat");
-            return PIPCK_OK;
-        }
-        const size_t lds = 4u * 64u * flat_pitch(run) * sizeof(uint16_t);
-        const bool no_pad = cpp == (len + 15) / 16 && len > 0;
-        uint32_t* q = (flags & kFlatQueue) && r1 >= 0 && no_pad ? launch_queue(as_stream(stream)) : nullptr;
-        if (q) {
-            // tasks of m ring batches each: the most packets that fit m*U rows, m
-            // batches ~ the default task length (>= one packet)
-            const uint32_t U = (uint32_t)fv->u;
-            uint32_t m = std::max(1u, (rows + U / 2) / U);
-            while (64u * U * m < cpp) m++;
-            const uint32_t run_c = std::min(kFlatMaxRun, (64u * U * m) / cpp);
-            const uint64_t tasks_c = (n + run_c - 1) / run_c;
-            if (tasks_c < (1ull << 34)) {
-                // one 4-wave block per SIMD slot the kernel's VGPRs allow: every wave resident
-                const uint32_t wps = U >= 32 ? 2u : U >= 24 ? 3u : 4u;
-                const uint64_t want = (uint64_t)device_cus() * wps;
-                const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (tasks_c + 3) / 4));
-                const size_t lds_c = 4u * 64u * flat_pitch(run_c) * sizeof(uint16_t);
-                hipLaunchKernelGGL(kFlatCont[r1][verify][nt_for(true)], dim3(grid), dim3(256), lds_c,
-                                   as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run_c, m, d_pseudo,
-                                   n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags, q);
-                PIPCK_LAUNCHED("k_flat_cont");
-                return PIPCK_OK;
-            }
-        }
         const uint32_t grid = grid_for(4, tasks, 0);
+        const size_t lds = 4u * 64u * flat_pitch(run) * sizeof(uint16_t);
         hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);

@@ -34,7 +34,8 @@ extern "C" {
  * small-kernel packets per lane (1 = 2, 2 = 4, 3 = 8, 4 = 16; default 2), bit 19 = mixed rows of
  * packed ragged tiles always find segments through LDS marks (default: a scalar
  * loop over up to 4 segment ends per row).  The packed-batch kernel
- * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32. */
+ * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32.
+ * Bit 20 = record the per-task timeline (pipck_trace_tasks below). */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the

@@ -260,48 +260,6 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
         engine.tune()
 
 
-@pytest.mark.parametrize("ring", [17, 25, 33])
-@pytest.mark.parametrize("rows", [0, 24, 40, 128])
-def test_persistent_flat_kernel_vs_oracle(oracle, ring, rows):
-    """k_flat_cont (tune flat_queue): a resident grid of waves claiming tasks
-    from per-XCD queue heads, one ring running across each wave's tasks.
-    Batch sizes from one packet (most waves find no task) to thousands of
-    tasks (stealing at the end), tasks of 1..64 packets, lengths ending
-    anywhere in their last chunk; strides with whole padding chunks take the
-    plain flat kernel.  Every launch must also leave its queue zeroed for the
-    next one on the stream, so the same shapes run twice."""
-    rng = np.random.default_rng(700 + ring + rows)
-    cases = [(1024, 1024), (1024, 1009), (1488, 1480), (1504, 1490), (2048, 2047), (8960, 8960), (8992, 8980),
-             (9216, 8980), (65536, 65535)]
-    try:
-        for stride, length in cases:
-            for n in sorted({1, 2, 63, 64, 65, int(rng.integers(100, 3000)), 40000 if stride < 20000 else 3000}):
-                engine.tune(0, ring, 0, nt_loads=True, rows_per_task=rows, flat_queue=True)
-                host = rng.integers(0, 256, n * stride, dtype=np.uint8)
-                if n > 2:
-                    host[stride:2 * stride] = 0xFF
-                    host[2 * stride:3 * stride] = 0
-                _, arena = upload(host, 0)
-                fam = int(rng.choice([0, 4, 6]))
-                seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
-                pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
-                want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
-                for _ in range(2):
-                    got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
-                    assert np.array_equal(got, want), (stride, length, n, np.nonzero(got != want)[0][:5])
-                ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
-                assert np.array_equal(ok.astype(bool), got == 0)
-                # explicit per-packet flows
-                if fam:
-                    flow_of = torch.from_numpy(rng.integers(0, N_FLOWS, n).astype(np.int32)).to(DEV)
-                    got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, flow_of, origin))
-                    ref = engine.tune(0, ring, 0, nt_loads=True, rows_per_task=rows)
-                    ref = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, flow_of, origin))
-                    assert np.array_equal(got, ref), (stride, length, n)
-    finally:
-        engine.tune()
-
-
 @pytest.mark.parametrize("ring,rows,nt", [(0, 0, True), (4, 4, True), (16, 64, True), (8, 2, False), (16, 8, True)])
 def test_tiny_stride_flat_kernel_vs_oracle(oracle, ring, rows, nt):
     """k_flat_tiny (8-byte-multiple strides 8..64 B, 16-byte-aligned arena;
