@@ -409,10 +409,19 @@ __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], buf_t tb, uint32_t
     for (int u = 0; u < U; u++) flat_load_row<NT>(v[u], tb, r0 + u * 64, lp, cpp, nch, lane);
 }
 
+// tune flags bit 24 (MEASUREMENT ONLY, wrong results): the flat kernel's
+// rows are waited for and consumed by one add each, with no per-packet
+// work, so tools can time the access pattern alone
+constexpr uint32_t kLoadsOnly = 1u << 24;
+
 // rs < tchunks (wave-uniform)
 __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
                                                 uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
-                                                uint16_t* part, uint32_t pitch, int lane) {
+                                                uint16_t* part, uint32_t pitch, int lane, uint32_t kflags) {
+    if (kflags & kLoadsOnly) {
+        acc += v.x;
+        return;
+    }
     if (pp.k == 0 && rs > 0) {  // previous packet ended exactly at the last row's end
         flat_stash(acc, pp.pkt - 1, part, pitch, lane);
         acc = 0;
@@ -440,11 +449,11 @@ __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uin
 template <int U>
 __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r0, uint32_t tchunks, RowPos& pp,
                                                  uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
-                                                 uint16_t* part, uint32_t pitch, int lane) {
+                                                 uint16_t* part, uint32_t pitch, int lane, uint32_t kflags) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t rs = r0 + u * 64;  // wave-uniform
-        if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+        if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane, kflags);
         pp.advance(cpp);
     }
 }
@@ -485,7 +494,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t rs = r0 + u * 64;  // wave-uniform
-                    if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                    if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane, kflags);
                     pp.advance(cpp);
                     flat_load_row<NT>(v[u], tb, rs + 64 * U, lp, cpp, nch, lane);  // unconditional (past the end: zeros)
                 }
@@ -503,7 +512,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const uint32_t rs = r0 + u * 64;  // < tchunks here
-                    flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                    flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane, kflags);
                     pp.advance(cpp);
                     flat_load_row<NT>(v[u], tb, rs + 64 * U, lp, cpp, nch, lane);
                 }
@@ -511,12 +520,12 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const uint32_t rs = r0 + u * 64;  // wave-uniform
-                if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                if (rs < tchunks) flat_reduce_row(v[u], rs, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane, kflags);
                 pp.advance(cpp);
             }
         } else {
             for (uint32_t r0 = 0; r0 < tchunks; r0 += 64 * U) {
-                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane);
+                flat_reduce_rows<U>(v, r0, tchunks, pp, acc, cpp, nch, tail, np, part, pitch, lane, kflags);
                 if (r0 + 64 * U < tchunks) flat_load_rows<U, NT>(v, tb, r0 + 64 * U, lp, cpp, nch, lane);
             }
         }

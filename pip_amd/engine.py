@@ -253,13 +253,13 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          packed_tiles: bool = True, wide_blocks: bool = False,
          small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True,
          flat_tiny: bool = True, force_flat_tiny: bool = False, packed_marks_only: bool = False,
-         trace: bool = False) -> None:
+         trace: bool = False, loads_only: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI."""
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
              | (0 if packed_tiles else 16) | (32 if wide_blocks else 0) | (0 if small else 64)
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
-             | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0)
+             | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 24 if loads_only else 0)
 )
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)

@@ -87,7 +87,7 @@ def main():
                     out = run()
                     if rnd == 0 and xcd == next(iter(arms)):
                         ref = out.clone()
-                    else:
+                    elif "probe" not in xcd:  # probe arms (e.g. loads_only) time a kernel that computes nothing
                         assert torch.equal(out, ref)
             for xcd, ms in res.items():
                 m = statistics.median(ms)
