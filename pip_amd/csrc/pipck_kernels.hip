@@ -331,8 +331,8 @@ constexpr uint32_t kFlatMaxRun = 64;  // packets per wave task
 __host__ __device__ constexpr uint32_t flat_pitch(uint32_t run) {
     return ((run + 1) / 2 % 2 ? (run + 1) / 2 : (run + 1) / 2 + 1) * 2;
 }
-__device__ __forceinline__ void flat_stash(uint64_t acc, uint32_t i, uint16_t* part, uint32_t pitch, int lane) {
-    part[lane * pitch + i] = (uint16_t)fold16(fold64(acc));
+__device__ __forceinline__ void flat_stash(uint32_t acc, uint32_t i, uint16_t* part, uint32_t pitch, int lane) {
+    part[lane * pitch + i] = (uint16_t)fold16(acc);
 }
 
 // Pseudo-header base of the task's packet `lane` (run <= 64), loaded when the
@@ -416,7 +416,7 @@ constexpr uint32_t kLoadsOnly = 1u << 24;
 
 // rs < tchunks (wave-uniform)
 __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
-                                                uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
+                                                uint32_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
                                                 uint16_t* part, uint32_t pitch, int lane, uint32_t kflags) {
     if (kflags & kLoadsOnly) {
         acc += v.x;
@@ -427,7 +427,7 @@ __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uin
         acc = 0;
     }
     if (pp.k + 65 <= nch) {  // wave-uniform: 64 whole data chunks of one packet, none its last
-        acc += sum4(v);
+        acc = dot4(v, acc);
         return;
     }
     uint32_t k = pp.k + lane;
@@ -435,20 +435,20 @@ __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uin
     u32x4 x = v;
     if (k >= nch || rs + lane >= tchunks) x = u32x4{0u, 0u, 0u, 0u};
     else if (k == nch - 1 && tail < 16) x = mask_tail(x, tail);
-    const uint64_t val = sum4(x);
+    const uint32_t val = dot4(x, 0u);
     const uint32_t b = cpp - pp.k;  // first lane holding the next packet
     if (b >= 64 || pp.pkt + 1 >= np) {
         acc += val;
     } else {
-        acc += lane < (int)b ? val : 0ull;
+        acc += lane < (int)b ? val : 0u;
         flat_stash(acc, pp.pkt, part, pitch, lane);
-        acc = lane < (int)b ? 0ull : val;
+        acc = lane < (int)b ? 0u : val;
     }
 }
 
 template <int U>
 __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r0, uint32_t tchunks, RowPos& pp,
-                                                 uint64_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
+                                                 uint32_t& acc, uint32_t cpp, uint32_t nch, int tail, uint32_t np,
                                                  uint16_t* part, uint32_t pitch, int lane, uint32_t kflags) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
         const uint32_t tchunks = np * cpp;
         // the task's chunks as a range-checked buffer (< 1 GiB: run <= 64, stride <= 16 MiB)
         const buf_t tb = buf_rsrc(reinterpret_cast<const u32x4*>(arena) + p0 * cpp, tchunks * 16u);
-        uint64_t acc = 0;
+        uint32_t acc = 0;  // 16-bit folds (v_dot2_u32_u16): <= 65 chunks of a packet per lane
         RowPos lp{0, 0}, pp{0, 0};
         const uint32_t fo = flat_flow_of(p0, np, pseudo, flow_of, lane);
         const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, fo, flow_origin, lane);
@@ -1434,9 +1434,9 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // packets: a ring of 24 over ~64-row tasks (cfg2 +0.7-1.4 % over 16 in
         // three scans; a ring of 32 cost it 8-15 %).  One task per wave either way.
         const bool jumbo = cpp >= 256;
+        const uint32_t flags = g_tune.flags.load();
         const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (jumbo ? 33u : 25u);
         const FlatVariant* fv = &flat_variant(loads);
-        const uint32_t flags = g_tune.flags.load();
         const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 128u : 64u);
         const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
