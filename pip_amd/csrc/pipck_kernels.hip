@@ -921,7 +921,7 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
 // Segment ends a mixed row walks in scalar code; beyond this many the row
 // finds its lanes' segments through LDS start marks instead.
 constexpr uint32_t kRowEndsLoop = 4;
-constexpr uint32_t kPackedMarksOnly = 1u << 19;  // pipck_tune flags bit 19: mixed rows always take the marks
+constexpr uint32_t kPackedMarksOnly = 1u << 19;  // pipck_tune flags bit 19: mixed rows always take the marks (k_packed: the end loop)
 
 // Reduce one row of a packed tile (every segment starts 16-byte aligned where
 // the previous one's chunks end).  Lane i of the wave holds segment i's start
@@ -1161,7 +1161,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
 // scan of the chunk counts, and streams the tile as a packed tile of
 // k_ragged.  Metadata per packet: 2 B + 1/8 B instead of a 16-byte
 // descriptor.  One tile per wave, one wave per block.
-template <bool VERIFY, int U, bool NT>
+template <bool VERIFY, int U, bool NT, bool MARKS>
 __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
                                                const uint64_t* __restrict__ tile_chunk, uint64_t n,
                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
@@ -1183,7 +1183,9 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
     const uint32_t nch = (len + 15) >> 4;
     const uint32_t excl = wave_incl_scan(nch) - nch;
     const uintptr_t addr = (uintptr_t)arena + 16ull * (tile_chunk[tile] + excl);
-    const uint32_t le_sum = ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len, nch, true, kflags);
+    // MARKS: the marks path compiled alone (the scalar end loop folded away)
+    const uint32_t le_sum =
+        ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len, nch, true, MARKS ? kflags | kPackedMarksOnly : kflags);
     if (valid) {
         const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
         const uint32_t P = pseudo ? Pbase + len : 0u;
@@ -1579,12 +1581,19 @@ template <bool V, int U>
 static void launch_packed_u(bool nt, uint64_t tiles, hipStream_t s, const uint8_t* a, const uint16_t* lens,
                             const uint64_t* tc, uint64_t n, const uint32_t* ps, uint32_t nf, const uint32_t* fo,
                             uint64_t origin, uint16_t* out, uint8_t* ok, uint32_t f) {
-    if (nt)
-        hipLaunchKernelGGL((k_packed<V, U, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf, fo,
-                           origin, out, ok, f);
+    const bool marks = (f & kPackedMarksOnly) != 0;
+    if (nt && marks)
+        hipLaunchKernelGGL((k_packed<V, U, true, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+                           fo, origin, out, ok, f);
+    else if (nt)
+        hipLaunchKernelGGL((k_packed<V, U, true, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+                           fo, origin, out, ok, f);
+    else if (marks)
+        hipLaunchKernelGGL((k_packed<V, U, false, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+                           fo, origin, out, ok, f);
     else
-        hipLaunchKernelGGL((k_packed<V, U, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf, fo,
-                           origin, out, ok, f);
+        hipLaunchKernelGGL((k_packed<V, U, false, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+                           fo, origin, out, ok, f);
 }
 
 static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
@@ -1608,20 +1617,25 @@ static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_len
         set_error("pipck_checksum_packed: more than 2^37 packets in one launch");
         return PIPCK_ERANGE;
     }
-    const uint32_t f = g_tune.flags.load();
+    // Mixed rows take the LDS-marks path by default here (tune flags bit 19
+    // selects the scalar end loop instead, the reverse of k_ragged), with a
+    // ring of 32 rows (154 VGPRs, still 3 waves/SIMD): cfg4 1.2618 vs 1.2814 ms and, at 16M
+    // packets, 2.448 vs 2.518 ms against the ring of 24 with the end loop, each
+    // alone gaining less (profiles/r02_knob_scan_cfg4_packed.jsonl).
+    const uint32_t f = g_tune.flags.load() ^ kPackedMarksOnly;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     const uint32_t nf = n_flows ? n_flows : 1u;
-    // rows in flight per wave: a ring of 24 by default (as k_ragged); 17/33 = 16/32
+    // rows in flight per wave: 17/25/33 = rings of 16/24/32
     switch (g_tune.loads.load()) {
         case 17: verify ? launch_packed_u<true, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
                         : launch_packed_u<false, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
                  break;
-        case 33: verify ? launch_packed_u<true, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
-                        : launch_packed_u<false, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
-                 break;
-        default: verify ? launch_packed_u<true, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
+        case 25: verify ? launch_packed_u<true, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
                         : launch_packed_u<false, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+                 break;
+        default: verify ? launch_packed_u<true, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
+                        : launch_packed_u<false, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
                  break;
     }
     PIPCK_LAUNCHED("k_packed");

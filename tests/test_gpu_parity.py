@@ -575,7 +575,7 @@ def test_packed_vs_oracle(oracle, shape, n):
     """pipck_checksum_packed / pipck_verify_packed (lengths + a per-64 index,
     no descriptors) against pip's algorithm, with implicit flows from an
     origin, explicit flow indices and no pseudo-header; both mixed-row paths
-    (scalar end loop, LDS marks)."""
+    (LDS marks, k_packed's default, and the scalar end loop: tune bit 19)."""
     rng = np.random.default_rng(hash((shape, n)) % 2**32)
     lens = _packed_lens(rng, shape, n, oracle)
     host, offs, arena, lens16, tc = _packed_upload(rng, lens)
