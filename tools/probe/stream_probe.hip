@@ -135,6 +135,46 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(wpe<U>
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
+// persistent coop: a resident grid of G blocks; block b takes block tasks
+// b, b+G, b+2G, ... (grid-stride, so the tasks in flight stay ~G wide) and each
+// wave's ring runs straight across them (no drain between tasks)
+__device__ __forceinline__ void gld_asm(u32x4& v, const uint8_t* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(v) : "v"(p));
+}
+template <int U>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wpe<U>()))) void k_coop_persist(
+    const uint8_t* __restrict__ a, uint64_t rows, uint32_t T, uint32_t* out) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = rfl(threadIdx.x >> 6);
+    const uint64_t bt = 4ull * T;                   // rows per block task
+    const uint64_t n_tasks = rows / bt;             // whole tasks only (the probe's sizes)
+    const uint64_t G = gridDim.x;
+    const uint64_t my_tasks = n_tasks > blockIdx.x ? (n_tasks - blockIdx.x + G - 1) / G : 0;
+    const uint64_t nr = my_tasks * T;               // this wave's rows over all its tasks
+    const uint32_t sh = __builtin_ctz(T);  // T: a power of two
+    auto addr = [&](uint64_t j) -> const uint8_t* {  // the wave's j-th row (past the end: row 0 again)
+        if (j >= nr) j = 0;
+        const uint64_t t = blockIdx.x + G * (j >> sh);
+        return a + ((t * bt) + w + 4 * (j & (T - 1))) * 1024 + lane * 16;
+    };
+    uint32_t acc = 0;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) gld_asm(v[u], addr(u));
+    for (uint64_t j = 0; j < nr; j += U) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v[u]) : "n"(U - 1));
+            acc += v[u].x + v[u].y + v[u].z + v[u].w;
+            gld_asm(v[u], addr(j + U + u));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]));
+#pragma unroll
+    for (int u = 1; u < U; u++) asm volatile("" : "+v"(v[u]));
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
 __global__ void k_fill(uint64_t* p, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         p[i] = (i * 0x9E3779B97F4A7C15ull) ^ (i >> 7);
@@ -159,6 +199,8 @@ static void launch(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out,
     } else if (m.kind == 1) {
         const uint32_t tc = WPB * m.T * 64 - g_skew;
         hipLaunchKernelGGL((k_coop<U, WPB>), dim3((uint32_t)((rows * 64 + tc - 1) / tc)), dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
+    } else if (m.kind == 5) {  // persistent coop: every wave slot the occupancy cap allows, 4-wave blocks
+        hipLaunchKernelGGL((k_coop_persist<U>), dim3(cus * wpe<U>()), dim3(256), 0, 0, a, rows, m.T, out);
     } else if (m.kind >= 10) {  // coop, rows in groups of G = kind - 10 (2, 4, 8, 16)
         const uint32_t tc = WPB * m.T * 64 - g_skew;
         const dim3 g((uint32_t)((rows * 64 + tc - 1) / tc));
@@ -196,7 +238,8 @@ int main(int argc, char** argv) {
         {"coop_u16_w4_t32", 16, 4, 32, 1},   {"coop_u32_w4_t64", 32, 4, 64, 1},   {"coop_u32_w4_t128", 32, 4, 128, 1},
         {"coop_u24_w2_t64", 24, 2, 64, 1},   {"coop_u24_w2_t128", 24, 2, 128, 1}, {"coop_u24_w4_t64_ovh24", 24, 4, 64, 3},
         {"coop_u24_w4_t64_ovh48", 24, 4, 64, 4}, {"coop_u24_w4_t64_g2", 24, 4, 64, 12}, {"coop_u24_w4_t64_g4", 24, 4, 64, 14},
-        {"coop_u24_w4_t64_g8", 24, 4, 64, 18}, {"coop_u24_w4_t64_g16", 24, 4, 64, 26}, {"coop_u16_w4_t64_ovh24", 16, 4, 64, 3}, {"coop_u16_w4_t64_ovh48", 16, 4, 64, 4},
+        {"coop_u24_w4_t64_g8", 24, 4, 64, 18}, {"coop_u24_w4_t64_g16", 24, 4, 64, 26},
+        {"coop_persist_u24_t64", 24, 4, 64, 5}, {"coop_persist_u24_t16", 24, 4, 16, 5}, {"coop_persist_u16_t64", 16, 4, 64, 5}, {"coop_u16_w4_t64_ovh24", 16, 4, 64, 3}, {"coop_u16_w4_t64_ovh48", 16, 4, 64, 4},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";
