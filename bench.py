@@ -25,7 +25,12 @@ roofline: algorithmic bytes per launch (L + 2 per packet: L read, u16 written)
 cpu_baseline: pip's own pip_inet_checksum / pip_ip_checksum (oracle/_ref,
           compiled from the reference) -- or the oracle's C restatement if
           _ref is absent -- on a bounded sample of the same packets, all host
-          cores and one core; rank 0, N=1.
+          cores and one core; rank 0, N=1.  Beside it ("chain"): the call pip's
+          TX path makes, pip_inet{,6}_checksum_buf on a header -> payload
+          pip_buf chain, over the same sample.
+roofline.traffic: PMC HBM bytes per launch from profiles/traffic_<cfg>.json,
+          attached only when that file was measured on the same kernel
+          instantiation (pipck_last_launch) of the same libpipck.so (sha256).
 """
 from __future__ import annotations
 
@@ -39,6 +44,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+import numpy as np  # noqa: E402
+
 from pip_amd import shard  # noqa: E402
 from pip_amd._lib import HDR_TCP, HDR_UDP  # noqa: E402
 from pip_amd.workloads import ALL, BY_CFG, N_FLOWS  # noqa: E402
@@ -46,8 +53,7 @@ from pip_amd.workloads import ALL, BY_CFG, N_FLOWS  # noqa: E402
 METRIC = "GiB/s payload checksummed (device-resident), MTU-9000 TCP batch; Mpkt/s"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PER_GPU_PACKETS = 8 << 20  # cfg5: 64M packets over 8 GPUs
-# the kernel each config's launch runs (a PMC traffic file applies to that kernel only)
-KERNEL_OF = {1: "k_small", 2: "k_flat<", 3: "k_flat<", 4: "k_packed", 5: "k_flat<"}
+LAUNCH_BOUND_S = 50e-6  # below this an event pair costs as much as the kernel (cfg1 at 1M headers)
 
 
 def parse(argv=None):
@@ -60,8 +66,44 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and host end-to-end legs")
     p.add_argument("--traffic", default="auto",
-                   help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json)")
+                   help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json); "
+                        "attached only if measured on this exact kernel of this exact libpipck.so build")
+    p.add_argument("--share-gpus", action="store_true",
+                   help="allow more ranks than visible GPUs (ranks then share devices; rehearsal only)")
     return p.parse_args(argv)
+
+
+def lib_sha256() -> str:
+    import hashlib
+
+    from pip_amd import _lib
+
+    return hashlib.sha256(Path(_lib.LIBPIPCK).read_bytes()).hexdigest()
+
+
+def last_kernel() -> str:
+    """The exact kernel instantiation the last batch launch on this thread ran (pipck_last_launch)."""
+    import ctypes as C
+
+    from pip_amd import _lib
+
+    buf = C.create_string_buffer(4096)
+    _lib.check("pipck_last_launch", _lib.load().pipck_last_launch(buf, len(buf)))
+    return buf.value.decode()
+
+
+def match_traffic(t: dict, kernel: str, lib_sha: str, algo_bytes: int, stride: int):
+    """A PMC traffic record applies to a bench line only if it was measured on the
+    same kernel instantiation (full demangled name), the same library build
+    (sha256 of libpipck.so), the same per-launch byte count and layout.
+    Returns (hbm bytes per launch or None, reason)."""
+    checks = (("kernel", t.get("kernel") == kernel), ("lib_sha256", t.get("lib_sha256") == lib_sha),
+              ("algorithmic_bytes_per_launch", t.get("algorithmic_bytes_per_launch") == algo_bytes),
+              ("arena_stride", t.get("arena_stride") == stride))
+    bad = [name for name, ok in checks if not ok]
+    if bad:
+        return None, "mismatch: " + ", ".join(bad)
+    return t.get("hbm_bytes_per_launch"), "match"
 
 
 def host_threads() -> int:
@@ -100,10 +142,19 @@ def run_rank(args) -> int:
 
     from pip_amd import engine
 
-    # one GPU per rank; ranks beyond the visible devices share them (rehearsing N>1 on a 1-GPU box)
-    n_dev = max(1, torch.cuda.device_count())
-    torch.cuda.set_device(env.local_rank % n_dev)
+    # one GPU per rank; more ranks than visible GPUs only with --share-gpus (a
+    # rehearsal), and never silently: the line then says the GPUs were shared
+    n_dev = torch.cuda.device_count()
+    try:
+        dev = shard.device_for_rank(env.local_rank, env.world, n_dev, args.share_gpus)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        shard.shutdown(env)
+        return 3
+    torch.cuda.set_device(dev)
     engine.require_gpu()
+    placement = {"rank": env.rank, "device": dev, "pci_bus_id": engine.pci_bus_id(dev),
+                 "name": torch.cuda.get_device_name(dev)}
     w = workload(args.workload)
     per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
     n_total = per_gpu * env.world
@@ -160,12 +211,14 @@ def run_rank(args) -> int:
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     shard.barrier(env)
+    kernel = last_kernel()  # the instantiation the timed launches ran
     elapsed = shard.max_over_ranks(env, t1 - t0)
     per_launch = sorted(s.elapsed_time(e) / 1e3 for s, e in zip(ev_s, ev_e))
     launch_s = per_launch[len(per_launch) // 2] if args.steps % 2 else \
         (per_launch[args.steps // 2 - 1] + per_launch[args.steps // 2]) / 2
     b2b_s = ev_s[0].elapsed_time(ev_e[-1]) / 1e3 / args.steps
     ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), t1 - t0, launch_s])
+    placements = shard.gather_objects(env, placement)
     total_bytes = sum(r[0] for r in ranks)
     total_pkts = sum(r[1] for r in ranks)
 
@@ -177,14 +230,17 @@ def run_rank(args) -> int:
     mpkt_s = total_pkts * args.steps / elapsed / 1e6
     algo_bytes = l4_bytes + 2 * count  # per launch on this rank
     achieved = algo_bytes / launch_s / 1e9
-    traffic = None
+    traffic, traffic_src, rocprof_ms = None, "none", None
+    sha = lib_sha256()
     tpath = Path(args.traffic) if args.traffic != "auto" else ROOT / "profiles" / f"traffic_cfg{w.cfg}.json"
     if args.traffic and tpath.exists():
         t = json.loads(tpath.read_text())
-        # only valid for the launch it was measured on: same kernel, layout and per-launch byte count
-        if (t.get("algorithmic_bytes_per_launch") == algo_bytes and t.get("arena_stride") == w.stride
-                and KERNEL_OF[w.cfg] in t.get("kernel", "")):
-            traffic = t.get("hbm_bytes_per_launch")
+        traffic, why = match_traffic(t, kernel, sha, algo_bytes, w.stride)
+        traffic_src = f"{tpath.relative_to(ROOT) if tpath.is_relative_to(ROOT) else tpath} ({why})"
+        if traffic is not None and t.get("rocprof_timed_median_ns"):
+            rocprof_ms = t["rocprof_timed_median_ns"] / 1e6
+    launch_bound = launch_s < LAUNCH_BOUND_S
+    n_shared = env.world - len({p["pci_bus_id"] for p in placements})
 
     line = {
         "metric": METRIC,
@@ -206,7 +262,8 @@ def run_rank(args) -> int:
             "l4_bytes_per_packet": w.length,
             "arena_stride": w.stride,
             "parallelism": f"{env.world} shard(s), contiguous packet ranges"
-                           f"{' of equal bytes' if w.ragged else ''}, no data-path collective",
+                           f"{' of equal bytes' if w.ragged else ''}, no data-path collective"
+                           f"{f', {env.world} ranks SHARING {env.world - n_shared} GPU(s) (--share-gpus)' if n_shared else ''}",
         },
         "mpkt_per_s": round(mpkt_s, 2),
         "per_gpu_gib_per_s": round(gib_s / env.world, 2),
@@ -214,6 +271,8 @@ def run_rank(args) -> int:
         "per_rank_gib_per_s": [round(r[0] * args.steps / r[2] / 2**30, 2) for r in ranks],
         "per_rank_packets": [int(r[1]) for r in ranks],
         "devices_visible": n_dev,
+        "distinct_gpus": env.world - n_shared,
+        "per_rank_device": placements,
         "l4_payload_gib_per_s": round(payload_gib_s, 2),
         "roofline": {
             "bound": "hbm",
@@ -227,9 +286,20 @@ def run_rank(args) -> int:
             "kernel_ms_min": round(per_launch[0] * 1e3, 4),
             "timing": "median of per-dispatch HIP event pairs on the launch stream",
             "algorithmic_bytes_per_launch": algo_bytes,
+            "kernel": kernel,
+            "lib_sha256": sha,
+            "traffic_source": traffic_src,
+            "launch_bound": launch_bound,
         },
         "cpu_baseline": None,
     }
+    if launch_bound:
+        # sub-50 us launches: the event pair and launch cost as much as the kernel;
+        # the rocprof trace of the same kernel and build is the kernel's own duration
+        line["roofline"]["timing"] += "; LAUNCH-BOUND at this size (kernel < 50 us): frac reflects launch overhead"
+        if rocprof_ms:
+            line["roofline"]["rocprof_kernel_ms"] = round(rocprof_ms, 5)
+            line["roofline"]["frac_rocprof"] = round(algo_bytes / (rocprof_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
 
     if env.rank == 0 and env.world == 1 and not args.no_cpu:
         line["cpu_baseline"], line["host_end_to_end"] = cpu_legs(args, w, out, count, first)
@@ -252,14 +322,38 @@ def _timed(run, threads, budget_s=3.0, max_reps=50):
             return reps, el
 
 
+def chain_leg(ref, w, arena, offs, lens, flows, first, threads, want):
+    """pip's TX call itself: pip_inet{,6}_checksum_buf on a header pip_buf chained to the payload
+    pip_buf (pip_tcp_packet.cpp:28-37 builds it, :124-134 checksums it; pip_udp.cpp the same with
+    8 bytes), over the same sample -- beside the flat pip_inet_checksum baseline."""
+    if ref is None or not w.family:
+        return None
+    hdr_len = {HDR_TCP: 20, HDR_UDP: 8}.get(w.hdr, 0)
+    chains = ref.tx_chains(arena, offs, lens, hdr_len)
+    try:
+        def run(t):
+            return chains.checksum(w.family, w.proto, flows, N_FLOWS, first, t)
+
+        ok = bool(np.array_equal(run(threads), want))
+        reps, el = _timed(run, threads)
+        reps1, el1 = _timed(run, 1, budget_s=1.0, max_reps=20)
+    finally:
+        chains.close()
+    l4 = int(lens.astype(np.int64).sum())
+    return {"call": f"pip_inet{'6' if w.family == 6 else ''}_checksum_buf on a {hdr_len}-B header pip_buf -> payload "
+                    "pip_buf chain, as pip's TX path builds and checksums it (pip_tcp_packet.cpp:28-37, 124-134; "
+                    "pip_checksum.cpp:90-148)",
+            "value": round(l4 * reps / el / 2**30, 3), "unit": "GiB/s", "cores": threads,
+            "single_core_gib_per_s": round(l4 * reps1 / el1 / 2**30, 3),
+            "mpkt_per_s": round(len(lens) * reps / el / 1e6, 2), "results_match_flat": ok}
+
+
 def cpu_legs(args, w, gpu_out, count, first):
     """pip's own checksum on the host cores over a bounded sample of the same
     packets (checked bit-exact against the GPU results), plus -- for fixed
     strides -- the PCIe-inclusive host -> device -> host rate of the same sample
     through pipck_host_checksum_fixed."""
     import ctypes as C
-
-    import numpy as np
 
     from oracle.oracle import Oracle, Reference
     from pip_amd import _lib
@@ -291,7 +385,8 @@ def cpu_legs(args, w, gpu_out, count, first):
                "sample": f"first {n} packets of the same Zipf workload ({l4 / 2**30:.2f} GiB of L4 bytes), "
                          f"pip_inet_checksum per packet, {reps} timed passes on {threads} threads; "
                          f"1 thread: {st:.3f} GiB/s",
-               "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified}
+               "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified,
+               "chain": chain_leg(ref, w, arena, offs, lens, flows, first, threads, res)}
         return cpu, {"value": None, "note": "host end-to-end is measured for fixed strides (pipck_host_checksum_fixed)"}
 
     # fixed strides: cfg1's whole 1M-header batch is a 20 MB sample; others ~2 GiB
@@ -315,6 +410,8 @@ def cpu_legs(args, w, gpu_out, count, first):
         mt = n * w.length * reps / el / 2**30
         reps1, el1 = _timed(run, 1, budget_s=1.0, max_reps=20)
         st = n * w.length * reps1 / el1 / 2**30
+        chain = chain_leg(ref, w, arena, np.arange(n, dtype=np.uint64) * w.stride, np.full(n, w.length, np.uint32),
+                          flows, first, threads, res)
 
         # host end-to-end: pinned host batch -> H2D -> kernel -> D2H (PCIe-bound)
         ctx = C.c_void_p()
@@ -339,7 +436,7 @@ def cpu_legs(args, w, gpu_out, count, first):
                      f"{reps} timed passes on {threads} threads; 1 thread: {st:.3f} GiB/s",
            "single_core_gib_per_s": round(st, 3),
            "mpkt_per_s": round(n * reps / el / 1e6, 2), "single_core_mpkt_per_s": round(n * reps1 / el1 / 1e6, 2),
-           "gpu_results_match": verified}
+           "gpu_results_match": verified, "chain": chain}
     e2e_d = {"value": round(e2e, 2), "unit": "GiB/s", "sample_packets": n, "pinned": True, "results_match": e2e_ok}
     return cpu, e2e_d
 

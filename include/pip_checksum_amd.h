@@ -73,8 +73,13 @@ void pip_checksum_amd_zero_copy(bool on);
 // Resident per-call service for this thread (pipck_ctx_zero_copy mode 3,
 // include/pipck.h): pip's synchronous calls are answered by a GPU block that
 // stays resident and polls a doorbell instead of a kernel launch per call.  The
-// block exits after 50 ms without a call and restarts on the next one.  Off by
-// default (auto mode); PIPCK_HOST_ZERO_COPY=3 turns it on for new threads.
+// block exits after 10 ms without a call and restarts on the next one.  Off by
+// default (auto mode); only this call turns it on (no environment variable).
+// WORST CASE: while the block runs, every hipFree / hipHostFree /
+// hipDeviceSynchronize anywhere in the process waits for it to exit, i.e. up
+// to 10 ms after this thread's last checksum call; pip_checksum_amd_resident
+// (false) ends it at once.  A latency path only: at ~7-9 us per call it cannot
+// beat pip's own ~0.5 us loop on a 1,480-B segment.
 void pip_checksum_amd_resident(bool on);
 
 // Capture mode for this thread: pip's UNCHANGED TX call sites become queue

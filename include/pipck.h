@@ -214,13 +214,19 @@ int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stri
 /* This context's per-packet path (pipck_host_sum): 0 = staged (H2D copy,
  * kernel, D2H copy), 1 = zero-copy (the kernel reads the pinned, coherent
  * staging buffer and writes the result to pinned host memory), 2 = auto
- * (zero-copy up to 64 KiB of staged bytes), 3 = resident (up to 64 KiB: one
- * 256-thread block of this context stays on the GPU, polls a doorbell in
- * pinned host memory and answers without a launch; it exits after 50 ms
- * without a call, or when the mode changes or the context is destroyed, and
- * relaunches on the next call; larger calls take the zero-copy launch).  A new
- * context starts in the mode the environment variable PIPCK_HOST_ZERO_COPY
- * (0..3) names, default 2.  Every path computes the same result. */
+ * (zero-copy up to 64 KiB of staged bytes; the mode of a new context),
+ * 3 = resident (up to 64 KiB: one 256-thread block of this context stays on
+ * the GPU, polls a doorbell in pinned host memory and answers without a
+ * launch; it exits after 10 ms without a call, or when the mode changes or
+ * the context is destroyed, and relaunches on the next call; larger calls take
+ * the zero-copy launch), 4 = resident with the doorbell in fine-grained device
+ * memory the host writes directly (large-BAR systems; falls back to mode 3's
+ * pinned doorbell where that allocation fails).  Every path computes the same
+ * result.  Nothing is read from the environment.
+ * WORST CASE of modes 3/4: while the resident block runs it holds one CU slot,
+ * and HIP makes every hipFree / hipHostFree / hipDeviceSynchronize in the
+ * whole process wait for it to exit -- up to 10 ms after this context's last
+ * call (the idle exit).  pipck_ctx_zero_copy(ctx, 2) ends it at once. */
 int pipck_ctx_zero_copy(pipck_ctx* ctx, int mode);
 void* pipck_host_alloc(size_t bytes);   /* pinned, coherent host memory (device-readable in place) */
 /* Pin an existing host range (a utun / socket buffer ring) so the GPU can read
@@ -272,6 +278,12 @@ int pipck_txq_add6_zc(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, uint8
  * without a copy.  Every in-place segment holds its pinned range until its
  * batch completes (see pipck_host_free). */
 int pipck_txq_auto_zero_copy(pipck_txq* q, int on);
+/* Largest flush (staged bytes + metadata) this queue runs in place: the
+ * kernels read the coherent pinned staging directly and write the results into
+ * it, with no copy command.  Larger flushes take one H2D and one D2H copy.
+ * Default 32 MiB (the measured crossover); 0 = always copy.
+ * Per queue; no environment variable changes it. */
+int pipck_txq_inplace_max(pipck_txq* q, uint64_t bytes);
 /* pip_ip_checksum (pip_checksum.cpp:35-39): an IPv4 header with ip_sum = 0 */
 int pipck_txq_add_ip(pipck_txq* q, const void* hdr, uint32_t len, void* csum_field);
 /* packets added since the last submit/flush */

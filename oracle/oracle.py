@@ -210,6 +210,10 @@ class Reference(_Common):
         _declare(self.lib, self.prefix)
         self.lib.ref_batch_fixed.argtypes = [_p, _u64, _u32, _u64, _i32, _u8, _p, _p, _u32, _u64, _p, _i32]
         self.lib.ref_batch_ragged.argtypes = [_p, _p, _p, _u64, _i32, _u8, _p, _p, _u32, _u64, _p, _i32]
+        self.lib.ref_chains_build.argtypes = [_p, _p, _p, _u64, _u32]
+        self.lib.ref_chains_build.restype = _p
+        self.lib.ref_chains_free.argtypes = [_p]
+        self.lib.ref_chains_checksum.argtypes = [_p, _i32, _u8, _p, _p, _u32, _u64, _p, _i32]
 
     @staticmethod
     def available() -> bool:
@@ -236,6 +240,11 @@ class Reference(_Common):
                                  max(n_flows, 1), flow_origin, _np_ptr(out), threads)
         return out
 
+    def tx_chains(self, arena: np.ndarray, offsets: np.ndarray, lens: np.ndarray, hdr_len: int) -> "RefChains":
+        """Each packet as pip's TX path builds it (pip_tcp_packet.cpp:28-37): a hdr_len-byte header
+        pip_buf chained to the payload pip_buf, both pointing into ``arena`` (which must outlive them)."""
+        return RefChains(self, arena, offsets, lens, hdr_len)
+
     def batch_ragged(self, arena: np.ndarray, offsets: np.ndarray, lens: np.ndarray, family: int, proto: int,
                      flows: bytes, n_flows: int, flow_origin: int = 0, threads: int = 1) -> np.ndarray:
         """pip_inet{,6}_checksum per packet of a ragged batch (pip_checksum.cpp:42-87)."""
@@ -247,3 +256,33 @@ class Reference(_Common):
                                   None if f4 is None else _np_ptr(f4), None if f6 is None else _np_ptr(f6),
                                   max(n_flows, 1), flow_origin, _np_ptr(out), threads)
         return out
+
+
+class RefChains:
+    """pip_buf chains built by pip's own code; ``checksum`` calls pip_inet{,6}_checksum_buf per packet
+    (pip_checksum.cpp:90-148) -- the call pip_tcp_packet.cpp:124-134 makes -- on ``threads`` threads."""
+
+    def __init__(self, ref: Reference, arena: np.ndarray, offsets: np.ndarray, lens: np.ndarray, hdr_len: int):
+        self.ref = ref
+        self._arena = arena
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        self.n = len(lens)
+        self.h = ref.lib.ref_chains_build(_np_ptr(arena), _np_ptr(offsets), _np_ptr(lens), self.n, hdr_len)
+
+    def checksum(self, family: int, proto: int, flows: bytes, n_flows: int, flow_origin: int = 0,
+                 threads: int = 1) -> np.ndarray:
+        out = np.zeros(self.n, dtype=np.uint16)
+        f4, f6 = Reference._flow_arrays(family, flows, n_flows)
+        self.ref.lib.ref_chains_checksum(self.h, family, proto, None if f4 is None else _np_ptr(f4),
+                                         None if f6 is None else _np_ptr(f6), max(n_flows, 1), flow_origin,
+                                         _np_ptr(out), threads)
+        return out
+
+    def close(self) -> None:
+        if self.h:
+            self.ref.lib.ref_chains_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

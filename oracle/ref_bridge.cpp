@@ -128,4 +128,59 @@ void ref_batch_ragged(const uint8_t* arena, const uint64_t* offsets, const uint3
     for (auto& x : th) x.join();
 }
 
+// CPU baseline of the call pip's TX path actually makes: pip_tcp_packet.cpp:28-37
+// builds each TCP segment as a chain -- a 20-byte header pip_buf, then the
+// payload pip_buf (pip_udp.cpp the same with an 8-byte UDP header) -- and
+// :124-134 checksums it with pip_inet{,6}_checksum_buf (pip_checksum.cpp:90-148),
+// which copies the shared_ptr and walks the chain, one pip_standard_checksum and
+// fold per segment.  The chains are built once (pip builds them while
+// constructing the packet) and point into the batch (pip_buf(p, len, 0): no
+// copy); ref_chains_checksum times the checksum calls alone.
+struct RefChains {
+    std::vector<std::shared_ptr<pip_buf>> head;
+};
+
+void* ref_chains_build(const uint8_t* arena, const uint64_t* offsets, const uint32_t* lens, uint64_t n,
+                       uint32_t hdr_len) {
+    auto* c = new RefChains();
+    c->head.reserve(n);
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t* p = arena + offsets[i];
+        const uint32_t h = lens[i] < hdr_len ? lens[i] : hdr_len;
+        auto head = std::make_shared<pip_buf>(p, h, 0);
+        if (lens[i] > h) head->set_next(std::make_shared<pip_buf>(p + h, lens[i] - h, 0));
+        c->head.push_back(std::move(head));
+    }
+    return c;
+}
+
+void ref_chains_free(void* h) { delete static_cast<RefChains*>(h); }
+
+void ref_chains_checksum(void* h, int family, uint8_t proto, const uint32_t* flows4, const uint8_t* flows6,
+                         uint32_t n_flows, uint64_t flow_origin, uint16_t* out, int threads) {
+    auto* c = static_cast<RefChains*>(h);
+    const uint64_t n = c->head.size();
+    if (threads < 1) threads = 1;
+    auto work = [&](uint64_t b, uint64_t e) {
+        for (uint64_t i = b; i < e; i++) {
+            const uint32_t f = (uint32_t)((flow_origin + i) % n_flows);
+            if (family == 4) {
+                pip_in_addr s, d;
+                s.s_addr = flows4[2 * f];
+                d.s_addr = flows4[2 * f + 1];
+                out[i] = pip_inet_checksum_buf(c->head[i], proto, s, d);
+            } else {
+                pip_in6_addr s, d;
+                std::memcpy(&s, flows6 + 32 * f, 16);
+                std::memcpy(&d, flows6 + 32 * f + 16, 16);
+                out[i] = pip_inet6_checksum_buf(c->head[i], proto, s, d);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; t++) th.emplace_back(work, n * t / threads, n * (t + 1) / threads);
+    work(0, n / threads);
+    for (auto& x : th) x.join();
+}
+
 }  // extern "C"

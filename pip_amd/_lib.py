@@ -87,12 +87,14 @@ SIGNATURES = {
     "pipck_txq_complete": (_i32, [_p]),
     "pipck_txq_inflight": (_u64, [_p]),
     "pipck_txq_auto_zero_copy": (_i32, [_p, _i32]),
+    "pipck_txq_inplace_max": (_i32, [_p, _u64]),
 }
 
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only
 INTERNAL_SIGNATURES = {
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
     "pipck_trace_tasks": (_i32, [_p, _u64]),
+    "pipck_last_launch": (_i32, [C.c_char_p, _sz]),
 }
 
 _lib = None

@@ -28,7 +28,8 @@ def _ctx() -> C.c_void_p:
 
 
 def set_zero_copy(mode: int) -> None:
-    """This thread's per-packet path: 0 staged, 1 zero-copy, 2 auto, 3 resident (pipck_ctx_zero_copy)."""
+    """This thread's per-packet path: 0 staged, 1 zero-copy, 2 auto, 3 resident, 4 resident with a device-memory
+    doorbell (pipck_ctx_zero_copy)."""
     call("pipck_ctx_zero_copy", _ctx(), mode)
 
 

@@ -26,14 +26,12 @@
 namespace pipck {
 
 static thread_local std::string t_err;
-// pipck_host_sum path of a new context: staged copies (0), zero-copy host
-// access (1), or auto (2: zero-copy up to kZeroCopyMax staged bytes); from
-// PIPCK_HOST_ZERO_COPY at creation, default auto; per context afterwards
-// (pipck_ctx_zero_copy).
-static int default_zero_copy() {
-    const char* e = getenv("PIPCK_HOST_ZERO_COPY");
-    return e && *e >= '0' && *e <= '3' ? *e - '0' : 2;
-}
+// pipck_host_sum path of a context: staged copies (0), zero-copy host access
+// (1), auto (2: zero-copy up to kZeroCopyMax staged bytes, the default of a
+// new context), or the resident service (3: doorbell in pinned host memory;
+// 4: doorbell in fine-grained device memory).  Set per context only
+// (pipck_ctx_zero_copy): nothing is read from the environment.
+constexpr int kDefaultZeroCopy = 2;
 constexpr size_t kZeroCopyMax = 64u << 10;
 void set_error(const std::string& msg) { t_err = msg; }
 
@@ -174,9 +172,9 @@ __global__ __launch_bounds__(1024) void k_exact_chain(const uint8_t* __restrict_
 // from the staging buffer.
 constexpr uint32_t kResidentInlineSegs = 5;
 // The doorbell -- host-written, device-polled.  In fine-grained device memory
-// when the host can write that directly (PIPCK_RESIDENT_VRAM=1: large-BAR
-// systems; the device then polls its own HBM), else in coherent pinned host
-// memory (each poll a PCIe read).
+// when the host can write that directly (mode 4: large-BAR systems; the device
+// then polls its own HBM), else in coherent pinned host memory (mode 3, and
+// mode 4 where that allocation fails; each poll a PCIe read).
 struct alignas(128) ResidentDoorbell {
     uint32_t req;    // host: sequence number of the posted request (written last)
     uint32_t nseg, init, pad0;
@@ -194,7 +192,12 @@ struct alignas(128) ResidentReply {
     uint32_t alive;  // 1 while the service runs
     uint32_t pad[29];
 };
-constexpr uint32_t kResidentIdleMs = 50;
+// Idle exit.  While the block runs it holds a CU slot, and every hipFree /
+// hipHostFree / device-wide synchronise in the process waits for it to exit:
+// this bounds that stall (idle time + one poll, ~10 ms) -- the worst case
+// pip_checksum_amd.h and pipck.h state.  A relaunch costs ~10 us, negligible
+// against 10 ms of idleness.
+constexpr uint32_t kResidentIdleMs = 10;
 
 __global__ __launch_bounds__(256) void k_resident(const ResidentDoorbell* db, ResidentReply* rp, uint64_t idle_ticks) {
     __shared__ uint64_t sa[64], sb[64];  // per segment (up to 64 in flight at once), then folded in order
@@ -381,8 +384,8 @@ struct pipck_ctx {
     uint32_t* d_pseudo = nullptr;
     void* d_flows = nullptr;
     uint32_t flows_cap = 0;
-    int zero_copy = 2;  // pipck_host_sum path (pipck_ctx_zero_copy)
-    // resident service (mode 3): its own stream, a mailbox in coherent pinned memory
+    int zero_copy = kDefaultZeroCopy;  // pipck_host_sum path (pipck_ctx_zero_copy)
+    // resident service (modes 3, 4): its own stream and mailbox
     hipStream_t res_stream = nullptr;
     ResidentDoorbell* db = nullptr;
     bool db_vram = false;
@@ -405,12 +408,11 @@ struct DeviceGuard {
     }
 };
 
-// Mode 3: make sure the resident block runs (launching it if it never ran or
-// has exited after its idle timeout).
+// Modes 3 and 4: make sure the resident block runs (launching it if it never
+// ran or has exited after its idle timeout).
 int resident_start(pipck_ctx* c) {
     if (!c->rp) {
-        const char* e = getenv("PIPCK_RESIDENT_VRAM");
-        c->db_vram = e && *e == '1' &&
+        c->db_vram = c->zero_copy == 4 &&
                      hipExtMallocWithFlags((void**)&c->db, sizeof(ResidentDoorbell), hipDeviceMallocFinegrained) == hipSuccess;
         if (!c->db_vram) PIPCK_HIP(hipHostMalloc((void**)&c->db, sizeof(ResidentDoorbell), hipHostMallocCoherent));
         for (size_t i = 0; i < sizeof(ResidentDoorbell) / 4; i++) ((volatile uint32_t*)c->db)[i] = 0;
@@ -503,7 +505,6 @@ int pipck_ctx_create(int device, pipck_ctx** out) {
     }
     pipck_ctx* c = new pipck_ctx();
     c->device = device;
-    c->zero_copy = default_zero_copy();
     for (int i = 0; i < 2; i++) {
         PIPCK_HIP(hipStreamCreateWithFlags(&c->stream[i], hipStreamNonBlocking));
         PIPCK_HIP(hipEventCreateWithFlags(&c->done[i], hipEventDisableTiming));
@@ -563,7 +564,7 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
     }
     hipStream_t s = c->stream[0];
     const int zc = c->zero_copy;
-    if (zc == 3 && need <= kZeroCopyMax) {
+    if (zc >= 3 && need <= kZeroCopyMax) {
         // the resident block: post the request, spin on its completion word
         if ((rc = resident_start(c))) return rc;
         ResidentDoorbell* db = c->db;
@@ -592,6 +593,10 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
                 // relaunch it (it resumes from `done`, so it serves this request)
                 if ((rc = resident_start(c))) return rc;
                 if (el > std::chrono::seconds(2)) {
+                    // end the block before returning: a block that starts late
+                    // would otherwise serve this stale request while the next
+                    // call rewrites the staging buffer and the doorbell
+                    resident_halt(c);
                     set_error("pipck_host_sum: the resident service did not answer within 2 s");
                     return PIPCK_EHIP;
                 }
@@ -636,13 +641,14 @@ int pipck_host_sum(pipck_ctx* c, const pipck_hseg* segs, uint32_t nseg, uint32_t
 }
 
 int pipck_ctx_zero_copy(pipck_ctx* c, int mode) {
-    if (!c || mode < 0 || mode > 3) {
-        set_error("pipck_ctx_zero_copy: null context or mode outside 0..3");
+    if (!c || mode < 0 || mode > 4) {
+        set_error("pipck_ctx_zero_copy: null context or mode outside 0..4");
         return PIPCK_EINVAL;
     }
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    if (mode != 3) resident_stop(c);  // release the resident block's CU slot
+    // any change releases the resident block's CU slot (3 <-> 4 also moves the doorbell)
+    if (mode != c->zero_copy) resident_stop(c);
     c->zero_copy = mode;
     return PIPCK_OK;
 }

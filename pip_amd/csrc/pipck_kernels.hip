@@ -33,8 +33,13 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
+#include <cxxabi.h>
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -409,10 +414,11 @@ __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], buf_t tb, uint32_t
     for (int u = 0; u < U; u++) flat_load_row<NT>(v[u], tb, r0 + u * 64, lp, cpp, nch, lane);
 }
 
-// tune flags bit 24 (MEASUREMENT ONLY, wrong results): the flat kernel's
+// tune flags bit 21 (MEASUREMENT ONLY, wrong results): the flat kernel's
 // rows are waited for and consumed by one add each, with no per-packet
-// work, so tools can time the access pattern alone
-constexpr uint32_t kLoadsOnly = 1u << 24;
+// work, so tools can time the access pattern alone.  (Bits 24..27 are the
+// small kernel's packets per lane: this bit must not overlap them.)
+constexpr uint32_t kLoadsOnly = 1u << 21;
 
 // rs < tchunks (wave-uniform)
 __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
@@ -1257,6 +1263,17 @@ struct Tune {
 };
 static Tune g_tune;
 
+// The batch kernel this thread launched last (its host-side handle), so a
+// measurement can name the exact template instantiation it timed
+// (pipck_last_launch in pipck_testing.h: bench.py binds a PMC traffic file to
+// that name).  One thread-local store per launch.
+static thread_local const void* t_last_kernel = nullptr;
+#define PIPCK_LAUNCH(K, ...)                                          \
+    do {                                                              \
+        t_last_kernel = reinterpret_cast<const void*>(K);             \
+        hipLaunchKernelGGL(K, __VA_ARGS__);                           \
+    } while (0)
+
 typedef void (*fixed_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
                          uint64_t, uint16_t*, uint8_t*);
 struct Variant {
@@ -1326,7 +1343,7 @@ static const SmallVariant kSmall[] = {PIPCK_S(2), PIPCK_S(4), PIPCK_S(8), PIPCK_
 #undef PIPCK_S
 #undef PIPCK_S1
 static const SmallVariant& small_variant() {
-    const uint32_t k = (g_tune.flags.load() >> 24) & 0xFu;
+    const uint32_t k = (g_tune.flags.load() >> 24) & 0xFu;  // bits 24..27 (kLoadsOnly is bit 21)
     return kSmall[k >= 1 && k <= 4 ? k - 1 : 0];
 }
 
@@ -1444,7 +1461,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
         const size_t lds = 4u * 64u * flat_pitch(run) * sizeof(uint16_t);
-        hipLaunchKernelGGL(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
+        PIPCK_LAUNCH(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");
@@ -1461,7 +1478,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : 64u;
         const uint32_t run = std::min(kFlatSmallMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
         const uint64_t tasks = (n + run - 1) / run;
-        hipLaunchKernelGGL(kFlatSmall[verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), 0,
+        PIPCK_LAUNCH(kFlatSmall[verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), 0,
                            as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
                            n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat_small");
@@ -1486,7 +1503,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t run = std::max(1u, std::min(kFlatTinyMaxRun / P, rows / G)) * P;
         const uint64_t tasks = (n + run - 1) / run;
         const size_t lds = 4u * tiny_wave_lds(hpp, run);
-        hipLaunchKernelGGL(kFlatTiny[ui][verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), lds,
+        PIPCK_LAUNCH(kFlatTiny[ui][verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), lds,
                            as_stream(stream), (const uint8_t*)d_arena, hpp, len, n, run, d_pseudo,
                            n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat_tiny");
@@ -1501,7 +1518,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (!g_tune.lanes.load() && !(g_tune.flags.load() & kNoSmall) && small_nl <= 4) {
         const SmallVariant& sv = small_variant();
         const uint64_t waves = (n + 64u * sv.k - 1) / (64u * sv.k);
-        hipLaunchKernelGGL(sv.fn[small_nl ? small_nl - 1 : 0][verify][nt_for(false)], dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0,
+        PIPCK_LAUNCH(sv.fn[small_nl ? small_nl - 1 : 0][verify][nt_for(false)], dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0,
                            as_stream(stream), (const uint8_t*)d_arena, stride, len, n, d_pseudo,
                            n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
         PIPCK_LAUNCHED("k_small");
@@ -1510,7 +1527,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     const uint32_t nch = (len + (aligned ? 0u : 15u) + 15u) / 16u;
     const Variant& v = pick_variant(nch);
     const uint32_t grid = grid_for(256 / v.g, n);
-    hipLaunchKernelGGL(v.fn[verify][nt_for(false)], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
+    PIPCK_LAUNCH(v.fn[verify][nt_for(false)], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
                        stride, len, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
     PIPCK_LAUNCHED("k_fixed");
     return PIPCK_OK;
@@ -1525,10 +1542,10 @@ static void launch_ragged_k(bool wide, uint64_t tiles, hipStream_t s, const uint
     // (runs of 2-4 consecutive tiles per wave measured 2-5 % slower,
     // profiles/r01_ragged_tpw_scan.jsonl)
     if (wide)
-        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(grid_for(4, tiles, 0)),
+        PIPCK_LAUNCH((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(grid_for(4, tiles, 0)),
                            dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
     else
-        hipLaunchKernelGGL((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(grid_for(1, tiles, 0)),
+        PIPCK_LAUNCH((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(grid_for(1, tiles, 0)),
                            dim3(64), 0, s, a, d, n, ps, out, fseg, ok, err, f);
 }
 
@@ -1583,16 +1600,16 @@ static void launch_packed_u(bool nt, uint64_t tiles, hipStream_t s, const uint8_
                             uint64_t origin, uint16_t* out, uint8_t* ok, uint32_t f) {
     const bool marks = (f & kPackedMarksOnly) != 0;
     if (nt && marks)
-        hipLaunchKernelGGL((k_packed<V, U, true, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+        PIPCK_LAUNCH((k_packed<V, U, true, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
                            fo, origin, out, ok, f);
     else if (nt)
-        hipLaunchKernelGGL((k_packed<V, U, true, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+        PIPCK_LAUNCH((k_packed<V, U, true, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
                            fo, origin, out, ok, f);
     else if (marks)
-        hipLaunchKernelGGL((k_packed<V, U, false, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+        PIPCK_LAUNCH((k_packed<V, U, false, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
                            fo, origin, out, ok, f);
     else
-        hipLaunchKernelGGL((k_packed<V, U, false, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
+        PIPCK_LAUNCH((k_packed<V, U, false, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
                            fo, origin, out, ok, f);
 }
 
@@ -1671,6 +1688,28 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
     g_tune.loads.store(loads_per_lane);
     g_tune.blocks.store(blocks);
     g_tune.flags.store(flags);
+}
+
+int pipck_last_launch(char* buf, size_t cap) {
+    // the handle of a __global__ function is a symbol with the kernel's own
+    // mangled name; demangled, it reads exactly as rocprofv3 names the kernel
+    if (!buf || !cap) return PIPCK_EINVAL;
+    buf[0] = 0;
+    Dl_info info;
+    if (!t_last_kernel || !dladdr(t_last_kernel, &info) || !info.dli_sname || info.dli_saddr != t_last_kernel) {
+        set_error("pipck_last_launch: no batch launch on this thread, or its symbol is not exported");
+        return PIPCK_EINVAL;
+    }
+    int st = 0;
+    char* dem = abi::__cxa_demangle(info.dli_sname, nullptr, nullptr, &st);
+    const char* name = st == 0 && dem ? dem : info.dli_sname;
+    const size_t len = std::strlen(name);
+    const int rc = len < cap ? PIPCK_OK : PIPCK_ERANGE;
+    std::memcpy(buf, name, std::min(len, cap - 1));
+    buf[std::min(len, cap - 1)] = 0;
+    std::free(dem);
+    if (rc) set_error("pipck_last_launch: buffer too small");
+    return rc;
 }
 
 int pipck_trace_tasks(void* d_buf, uint64_t cap) {

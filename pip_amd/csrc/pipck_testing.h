@@ -4,12 +4,14 @@
  * include/pipck.h: it is process-global mutable state that changes kernel
  * selection for every context and thread, so a product caller must never
  * use it.  Every setting computes the same results (the GPU tests sweep them
- * against the oracle); only speed changes.  pipck_tune(0, 0, 0, 0) restores
+ * against the oracle); only speed changes -- except bit 21 below, a
+ * measurement-only probe.  pipck_tune(0, 0, 0, 0) restores
  * the automatic choice.
  */
 #ifndef PIPCK_TESTING_H
 #define PIPCK_TESTING_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -35,7 +37,10 @@ extern "C" {
  * packed ragged tiles always find segments through LDS marks (default: a scalar
  * loop over up to 4 segment ends per row).  The packed-batch kernel
  * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32.
- * Bit 20 = record the per-task timeline (pipck_trace_tasks below). */
+ * Bit 20 = record the per-task timeline (pipck_trace_tasks below).  Bit 21 =
+ * MEASUREMENT ONLY, WRONG RESULTS: the flat-stream kernel waits for and
+ * consumes every row with one add and does no per-packet work (times the
+ * access pattern alone).  Bits 22, 23 and 28..31 are unused. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the
@@ -44,6 +49,13 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
  * (100 MHz s_memrealtime clock) into d_buf[task] for task < cap.  d_buf is
  * device memory; null switches recording off. */
 int pipck_trace_tasks(void* d_buf, uint64_t cap);
+
+/* The demangled name of the batch kernel the calling thread launched last --
+ * the exact template instantiation, spelled as rocprofv3 names it (e.g.
+ * "void pipck::k_flat<32, true, false, true, 4>(unsigned char const*, ...)").
+ * bench.py attaches a PMC traffic file to a bench line only when the file was
+ * measured on this kernel of this build.  PIPCK_EINVAL before any launch. */
+int pipck_last_launch(char* buf, size_t cap);
 
 #ifdef __cplusplus
 }

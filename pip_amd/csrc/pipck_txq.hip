@@ -13,7 +13,6 @@
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
 
-#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -133,6 +132,14 @@ struct TxBatch {
 
 using namespace pipck;
 
+// A flush whose staged bytes + metadata fit 32 MiB runs without any copy
+// command: the kernels read the coherent pinned staging in place and write the
+// results into it.  Measured on one producer thread (tools/txq_bench.cpp,
+// profiles/r01_txq_inplace_ab.jsonl): a 64-packet flush 40 vs 50 us, 1,024
+// packets 0.10 vs 0.12 ms, pipelined 16K-packet batches +15 %.  Larger batches
+// keep the H2D / D2H copies.  Per queue: pipck_txq_inplace_max.
+constexpr uint64_t kInPlaceFlushMax = 32u << 20;
+
 struct pipck_txq {
     pipck_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
@@ -140,6 +147,7 @@ struct pipck_txq {
     int device = 0;
     TxBatch batch[2];
     bool auto_zc = false;      // plain adds read pinned segments in place (pipck_txq_auto_zero_copy)
+    uint64_t inplace_max = kInPlaceFlushMax;  // pipck_txq_inplace_max
     int cur = 0;         // batch receiving adds
     bool inflight = false;  // batch[cur ^ 1] has been submitted and not completed
 };
@@ -191,13 +199,20 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
         }
     }
     TxBatch* b = &q->batch[q->cur];
-    const size_t seg0 = b->inet_segs.size(), bytes0 = b->bytes.size;
+    const size_t seg0 = b->inet_segs.size(), bytes0 = b->bytes.size, held0 = b->held.size();
+    // a refused packet leaves the batch as it was: its segments, bytes and the
+    // pinned-range holds taken for it are all dropped
+    auto rollback = [&] {
+        b->inet_segs.resize(seg0);
+        b->bytes.size = bytes0;
+        for (size_t h = held0; h < b->held.size(); h++) pinned_release(*b->held[h]);
+        b->held.resize(held0);
+    };
     for (uint32_t i = 0; i < nseg; i++) {
         const bool in_place = (zc || q->auto_zc) && segs[i].len && hold_pinned(b, segs[i].ptr, segs[i].len);
         if (zc && segs[i].len && !in_place) {
             // the GPU would read it in place: it must be pinned; drop this packet's segments
-            b->inet_segs.resize(seg0);
-            b->bytes.size = bytes0;
+            rollback();
             set_error("pipck_txq_add_zc: segment outside every range from pipck_host_alloc / "
                       "pipck_host_register");
             return PIPCK_EINVAL;
@@ -211,8 +226,7 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
         uint64_t off = 0;
         int rc = append_bytes(b, segs[i].ptr, segs[i].len, &off);
         if (rc) {
-            b->inet_segs.resize(seg0);
-            b->bytes.size = bytes0;
+            rollback();
             return rc;
         }
         b->inet_segs.push_back(pipck_desc{off, segs[i].len, 0});
@@ -221,17 +235,6 @@ int add_inet(pipck_txq* q, const pipck_hseg* segs, uint32_t nseg, const TxPseudo
     b->inet_pseudo.push_back(ps);
     b->inet_field.push_back((uint8_t*)field);
     return PIPCK_OK;
-}
-
-// A flush whose staged bytes + metadata fit 32 MiB runs without any copy
-// command: the kernels read the coherent pinned staging in place and write the
-// results into it.  Measured on one producer thread (tools/txq_bench.cpp,
-// profiles/r01_txq_inplace_ab.jsonl): a 64-packet flush 40 vs 50 us, 1,024
-// packets 0.10 vs 0.12 ms, pipelined 16K-packet batches +15 %.  Larger batches
-// keep the H2D / D2H copies.
-static size_t in_place_flush_max() {  // read per flush: tests and A/Bs switch it at run time
-    const char* e = getenv("PIPCK_TXQ_INPLACE_MAX");  // bytes; 0 = always copy
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(32u << 20);
 }
 
 // Enqueue batch b on the queue's stream: H2D of bytes + metadata (or nothing,
@@ -250,7 +253,7 @@ int enqueue(pipck_txq* q, TxBatch* b) {
     int rc = b->meta.reserve(meta_all);
     if (rc) return rc;
     const size_t nb = al(b->bytes.size);
-    const bool in_place = nb + meta_all <= in_place_flush_max();
+    const bool in_place = nb + meta_all <= q->inplace_max;
     uint8_t* d_bytes = nullptr;
     if (in_place) {
         if ((rc = b->bytes.reserve(16))) return rc;  // a valid base even for an empty batch
@@ -365,6 +368,15 @@ int pipck_txq_auto_zero_copy(pipck_txq* q, int on) {
     return PIPCK_OK;
 }
 
+int pipck_txq_inplace_max(pipck_txq* q, uint64_t bytes) {
+    if (!q) {
+        set_error("pipck_txq_inplace_max: null queue");
+        return PIPCK_EINVAL;
+    }
+    q->inplace_max = bytes;
+    return PIPCK_OK;
+}
+
 int pipck_txq_destroy(pipck_txq* q) {
     if (!q) return PIPCK_OK;
     if (q->stream) {
@@ -454,7 +466,10 @@ int pipck_txq_submit(pipck_txq* q) {
         int rc = complete_inflight(q);  // at most one batch in flight
         if (rc) return rc;
         TxBatch* b = &q->batch[q->cur];
-        if (!b->pending()) return PIPCK_OK;
+        if (!b->pending()) {
+            b->clear();  // nothing queued: nothing may stay held either
+            return PIPCK_OK;
+        }
         if ((rc = enqueue(q, b))) return rc;
         q->inflight = true;
         q->cur ^= 1;

@@ -42,6 +42,21 @@ def require_gpu() -> None:
     load()
 
 
+def pci_bus_id(device: int) -> str:
+    """PCI bus id of a HIP device ("0000:05:00.0"), from hipDeviceGetPCIBusId: names the physical
+    GPU a rank ran on (bench.py's per_rank_device)."""
+    buf = C.create_string_buffer(64)
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        if hip.hipDeviceGetPCIBusId(buf, C.c_int(len(buf)), C.c_int(device)) == 0:
+            return buf.value.decode()
+    except OSError:
+        pass
+    p = _torch().cuda.get_device_properties(device)
+    return f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:" \
+           f"{getattr(p, 'pci_device_id', 0):02x}.0"
+
+
 # ---------------------------------------------------------------- flows
 def gen_flows(family: int, n_flows: int, seed: int, proto: int, device=None):
     """Synthetic flow table on the device + its pseudo-header bases."""
@@ -148,22 +163,30 @@ def packed_index(lens, n: int | None = None):
     return tc
 
 
-_packed_ok: dict = {}
+_packed_total: dict = {}  # id(tile_chunk) -> (weakref, tensor version, n, chunks)
 
 
 def _check_packed(arena, lens, tile_chunk, n):
-    """Host-side guard (once per index tensor): the batch must lie inside the arena."""
+    """Host-side guard: the batch must lie inside the arena.  The index's total
+    (tile_chunk[ceil(n/64)], one device read) is cached on the index tensor
+    OBJECT and its in-place version counter, never on addresses: a freed tensor's
+    address is reused by the caching allocator, and a pointer-keyed cache would
+    then skip the check for a larger batch.  The bound itself is re-checked
+    against the arena on every call."""
+    import weakref
+
     if n > lens.numel() or tile_chunk.numel() < (n + 63) // 64 + 1:
         raise ValueError("lens / tile_chunk shorter than the batch")
-    key = (tile_chunk.data_ptr(), n, arena.data_ptr(), arena.numel())
-    if key in _packed_ok:
-        return
-    chunks = int(tile_chunk[(n + 63) // 64].item())
+    ent = _packed_total.get(id(tile_chunk))
+    if ent is not None and ent[0]() is tile_chunk and ent[1] == tile_chunk._version and ent[2] == n:
+        chunks = ent[3]
+    else:
+        chunks = int(tile_chunk[(n + 63) // 64].item())
+        if len(_packed_total) > 64:
+            _packed_total.clear()
+        _packed_total[id(tile_chunk)] = (weakref.ref(tile_chunk), tile_chunk._version, n, chunks)
     if 16 * chunks > arena.numel() * arena.element_size():
         raise ValueError(f"packed batch needs {16 * chunks} B, arena has {arena.numel() * arena.element_size()}")
-    if len(_packed_ok) > 64:
-        _packed_ok.clear()
-    _packed_ok[key] = True
 
 
 def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
@@ -255,11 +278,13 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          flat_tiny: bool = True, force_flat_tiny: bool = False, packed_marks_only: bool = False,
          trace: bool = False, loads_only: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
-    (pip_amd/csrc/pipck_testing.h), not part of the public ABI."""
+    (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
+    except loads_only (bit 21), a measurement-only probe of the flat kernel's access pattern."""
+    if not 0 <= small_k_log <= 4:
+        raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
              | (0 if packed_tiles else 16) | (32 if wide_blocks else 0) | (0 if small else 64)
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
-             | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 24 if loads_only else 0)
-)
+             | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)

@@ -121,6 +121,19 @@ def byte_cuts(prefix_bytes, world: int) -> list[int]:
     return cuts
 
 
+def device_for_rank(local_rank: int, world: int, n_devices: int, share: bool = False) -> int:
+    """One GPU per rank: rank r takes device r.  More ranks than visible GPUs is
+    refused unless ``share`` (a rehearsal of N>1 on fewer GPUs, which the bench
+    line then reports as shared) -- so an N-GPU line can never silently claim
+    GPUs it did not run on."""
+    if n_devices < 1:
+        raise ValueError("no visible GPU")
+    if world > n_devices and not share:
+        raise ValueError(f"{world} ranks but only {n_devices} visible GPU(s); pass --share-gpus to let ranks "
+                         "share devices (the line then says so)")
+    return local_rank % n_devices
+
+
 def init_control_plane(env: DistEnv) -> None:
     """gloo process group for the barrier and the MAX of elapsed times."""
     if not env.distributed:
@@ -172,6 +185,17 @@ def gather_over_ranks(env: DistEnv, values: list[float]) -> list[list[float]]:
     out = [torch.empty_like(t) for _ in range(env.world)]
     dist.all_gather(out, t)
     return [o.tolist() for o in out]
+
+
+def gather_objects(env: DistEnv, obj) -> list:
+    """Every rank's picklable ``obj`` (small control records), indexed by rank."""
+    if not env.distributed:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * env.world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def shutdown(env: DistEnv) -> None:

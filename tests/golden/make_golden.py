@@ -9,8 +9,13 @@ Writes
   kat.json            known-answer vectors: inputs (hex or a byte pattern) and the
                       results of pip's own functions (pip/pip_checksum.cpp:9-148)
   batches.json        per BASELINE.json config, a reduced batch made by the
-                      generator spec (oracle/pipck_oracle.c): sha256 of the arena
-                      bytes, and sha256 + head of pip's results over it
+                      generator spec (oracle/pipck_oracle.c) in the layout the
+                      product runs it in (cfg1 packed at a 20-B stride; cfg4's
+                      arena is also the packed-lengths layout): sha256 of the
+                      arena bytes, and sha256 + head of pip's results over it;
+                      plus "edge_*" batches whose results include pip's 0x0000
+                      and 0xFFFF corners (EDGES below), so the fold edge is pinned
+                      through every batch kernel, not only through the KATs
   stack_replay.txt    every IP packet pip's real stack emits for the scripted
                       exchange in oracle/stack_replay.cpp (link-substitution test)
 
@@ -156,6 +161,113 @@ def sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+# Edge batches: a config's generated batch with some packets made to hit pip's
+# fold corners.  "ck_every"/"ck_off": packet i (i % ck_every == 0) gets pip's
+# own checksum of the unpatched packet stored big-endian at ck_off (its
+# th_sum / uh_sum / ip_sum, zero in the generated bytes) -> that packet now
+# checksums to 0x0000.  "zero_every": packet i (i % zero_every == 1) becomes all
+# zero bytes -> 0xFFFF where there is no pseudo-header (pip_ip_checksum of an
+# all-zero header).  "zero_flows_every": flow records k % zero_flows_every == 0
+# get zero addresses; with proto 0 and length 0 (an empty segment) their total
+# is 0 and pip returns 0xFFFF under a pseudo-header.  Each spec names the batch
+# kernel it exercises (tests/test_gpu_parity.py checks pipck_last_launch).
+EDGES = {
+    "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat<24,"},
+    "edge_flat32_udp6": {"cfg": 3, "n": 48, "ck_every": 2, "ck_off": 6, "kernel": "k_flat<32,"},
+    "edge_small_ip20": {"cfg": 1, "n": 4096, "ck_every": 5, "ck_off": 10, "zero_every": 7, "kernel": "k_small<"},
+    "edge_packed_tcp4": {"cfg": 4, "n": 4096, "ck_every": 2, "ck_off": 16, "zero_every": 0, "kernel": "k_packed<"},
+    "edge_flat_len0_v4": {"cfg": 2, "n": 256, "stride": 1024, "length": 0, "proto": 0, "zero_flows_every": 4,
+                          "kernel": "k_flat<24,"},
+}
+
+
+def edge_inputs_cpu(orc, b: dict):
+    """Rebuild an edge fixture's inputs on the CPU from its record (generator twin +
+    the recorded patches / zeroed flows): (arena, offsets, lengths, flow table bytes)."""
+    w = next(x for x in ALL.values() if x.cfg == b["cfg"])
+    n, fam = b["n"], b["family"]
+    flows = bytearray(orc.flows_table(fam, b["seed"], b["n_flows"], b["proto"]) if fam else b"")
+    rec = 12 if fam == 4 else 36
+    for k in b["zero_flows"]:
+        flows[rec * k:rec * k + rec - 4] = bytes(rec - 4)
+    if w.ragged:
+        arena, offs, lens = orc.gen_ragged_batch(b["seed"], b["first"], n, b["hdr"])
+    else:
+        st, L = b["stride"], b["length"]
+        arena = orc.gen_fixed_batch(b["seed"], b["first"], n, L, b["hdr"], st) if L else np.zeros(n * st, np.uint8)
+        offs, lens = np.arange(n, dtype=np.uint64) * st, np.full(n, L, dtype=np.uint32)
+    for o, hx in b["patches"]:
+        v = bytes.fromhex(hx)
+        arena[o:o + len(v)] = np.frombuffer(v, dtype=np.uint8)
+    return arena, offs, lens, bytes(flows)
+
+
+def oracle_edge_results(orc, b: dict, arena, offs, lens, flows: bytes) -> np.ndarray:
+    """The oracle restatement, packet by packet, over an edge batch (its flow table may differ
+    from the generator's, so the batch helpers that derive flows from the seed do not apply)."""
+    fam, rec = b["family"], (12 if b["family"] == 4 else 36)
+    out = np.zeros(b["n"], dtype=np.uint16)
+    for i in range(b["n"]):
+        o, L = int(offs[i]), int(lens[i])
+        data = arena[o:o + L].tobytes()
+        if not fam:
+            out[i] = orc.ip_checksum(data)
+        else:
+            r = flows[rec * ((b["first"] + i) % b["n_flows"]):][:rec - 4]
+            half = (rec - 4) // 2
+            out[i] = (orc.inet_checksum if fam == 4 else orc.inet6_checksum)(data, b["proto"], r[:half], r[half:], L)
+    return out
+
+
+def edge_batch(orc, ref, name: str, spec: dict) -> dict:
+    """Build one edge batch with pip's own code; return its fixture record."""
+    w = next(x for x in ALL.values() if x.cfg == spec["cfg"])
+    n, first = spec["n"], 0
+    proto = spec.get("proto", w.proto)
+    fam = w.family
+    flows = bytearray(orc.flows_table(fam, w.seed, N_FLOWS, proto) if fam else b"")
+    rec = 12 if fam == 4 else 36
+    zero_flows = list(range(0, N_FLOWS, spec["zero_flows_every"])) if spec.get("zero_flows_every") else []
+    for k in zero_flows:
+        flows[rec * k:rec * k + rec - 4] = bytes(rec - 4)  # src, dst (proto stays)
+    flows = bytes(flows)
+    if w.ragged:
+        arena, offs, lens = orc.gen_ragged_batch(w.seed, first, n, w.hdr)
+        stride, length = 0, None
+    else:
+        stride, length = spec.get("stride", w.stride), spec.get("length", w.length)
+        arena = orc.gen_fixed_batch(w.seed, first, n, length, w.hdr, stride) if length else \
+            np.zeros(n * stride, dtype=np.uint8)
+        offs = np.arange(n, dtype=np.uint64) * stride
+        lens = np.full(n, length, dtype=np.uint32)
+
+    def pip_results(a):
+        if w.ragged:
+            return ref.batch_ragged(a, offs, lens, fam, proto, flows, N_FLOWS, first)
+        return ref.batch_fixed(a, stride, length, n, fam, proto, flows, N_FLOWS, first)
+
+    base = pip_results(arena)
+    patches = []
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        if spec.get("zero_every") and i % spec["zero_every"] == 1:
+            patches.append([o, "00" * L])
+        elif spec.get("ck_every") and i % spec["ck_every"] == 0 and L >= spec["ck_off"] + 2:
+            patches.append([o + spec["ck_off"], int(base[i]).to_bytes(2, "big").hex()])
+    for o, hx in patches:
+        b = bytes.fromhex(hx)
+        arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    out = pip_results(arena)
+    rec_ = {"n": n, "first": first, "family": fam, "proto": proto, "n_flows": N_FLOWS}
+    assert np.array_equal(oracle_edge_results(orc, rec_, arena, offs, lens, flows), out), name
+    n_zero, n_ffff = int((out == 0).sum()), int((out == 0xFFFF).sum())
+    assert n_zero + n_ffff > 0, name
+    return {"cfg": w.cfg, "n": n, "first": first, "seed": w.seed, "stride": stride, "length": length, "hdr": w.hdr,
+            "family": fam, "proto": proto, "n_flows": N_FLOWS, "zero_flows": zero_flows, "patches": patches,
+            "kernel": spec["kernel"], "arena_sha256": sha(arena), "results_sha256": sha(out.astype("<u2")),
+            "head": [int(x) for x in out[:16]], "n_zero": n_zero, "n_ffff": n_ffff}
+
+
 def main() -> None:
     ref, orc = Reference(), Oracle()
     rng = random.Random(20261015)
@@ -194,6 +306,9 @@ def main() -> None:
                          "head": [int(x) for x in ref_out[:16]], "n_zero": int((ref_out == 0).sum()),
                          "n_ffff": int((ref_out == 0xFFFF).sum()), **extra}
         print(name, n, batches[name]["results_sha256"][:16])
+    for name, spec in EDGES.items():
+        batches[name] = edge_batch(orc, ref, name, spec)
+        print(name, batches[name]["n"], "zero", batches[name]["n_zero"], "ffff", batches[name]["n_ffff"])
     (OUT / "batches.json").write_text(json.dumps(batches, indent=1))
 
     out = subprocess.run([str(ROOT / "oracle" / "_ref" / "stack_replay_ref")], check=True, capture_output=True,

@@ -44,7 +44,7 @@ def test_libpipck_exports_every_declared_function():
 
 def test_internal_tuning_hook_is_outside_the_public_header():
     internal = header_functions(ROOT / "pip_amd" / "csrc" / "pipck_testing.h")
-    assert internal == sorted(_lib.INTERNAL_SIGNATURES) == ["pipck_trace_tasks", "pipck_tune"]
+    assert internal == sorted(_lib.INTERNAL_SIGNATURES) == ["pipck_last_launch", "pipck_trace_tasks", "pipck_tune"]
     for f in internal:
         assert f in dynsyms(_lib.LIBPIPCK)  # still exported, for tests/ and tools/
 
@@ -62,8 +62,25 @@ def test_public_header_has_no_process_global_knobs():
             else:  # the drop-in's switches are per calling thread (thread_local queue)
                 assert name.startswith("pip_checksum_amd_"), name
         assert "pipck_tune" not in text and "pipck_host_zero_copy" not in text
-    shim = (ROOT / "pip_amd" / "csrc" / "pip_checksum_shim.cpp").read_text()
-    assert "getenv" not in shim and "PIPCK_TXQ_AUTO_ZERO_COPY" not in (ROOT / "pip_amd" / "csrc" / "pipck_txq.hip").read_text()
+
+
+def test_product_sources_read_no_environment():
+    """No product source reads a knob from the environment: every mode is a
+    per-context / per-queue call.  The internal tuning
+    hook (pipck_testing.h) is the only process-global switch, and it is not
+    read from the environment either."""
+    csrc = ROOT / "pip_amd" / "csrc"
+    files = sorted(csrc.glob("*.hip")) + sorted(csrc.glob("*.cpp")) + sorted(csrc.glob("*.hpp")) + \
+        sorted((ROOT / "include").glob("*.h"))
+    assert len(files) >= 9
+    for f in files:
+        code = re.sub(r"/\*.*?\*/|//[^\n]*", "", f.read_text(), flags=re.S)
+        assert not re.search(r"\b(getenv|secure_getenv|environ)\b", code), f.name
+    # and the documented knobs that used to be environment variables are gone from the headers
+    for h in ("pipck.h", "pip_checksum_amd.h"):
+        text = (ROOT / "include" / h).read_text()
+        for knob in ("PIPCK_HOST_ZERO_COPY", "PIPCK_RESIDENT_VRAM", "PIPCK_TXQ_INPLACE_MAX"):
+            assert knob not in text, (h, knob)
 
 
 def test_libpipck_loads_and_reports_version():

@@ -9,7 +9,9 @@ to 0xFFFF, i.e. recompute to 0x0000 and verify as valid).
 """
 import ctypes as C
 import hashlib
+import json
 import threading
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -94,25 +96,28 @@ def test_every_known_answer_on_gpu_zero_copy(kat):
         pc.set_zero_copy(2)
 
 
-def test_every_known_answer_on_gpu_resident(kat):
+@pytest.mark.parametrize("mode", [3, 4])
+def test_every_known_answer_on_gpu_resident(kat, mode):
     """The same known answers through the resident service (mode 3: one block
-    stays on the GPU polling a doorbell; requests over 64 KiB -- the 131,076-B
-    wrap KATs -- take the zero-copy launch).  The block's idle exit and
-    relaunch are exercised too: a pause longer than its 50 ms idle timeout,
-    then more calls."""
+    stays on the GPU polling a doorbell in pinned host memory; mode 4: the
+    doorbell in fine-grained device memory; requests over 64 KiB -- the
+    131,076-B wrap KATs -- take the zero-copy launch).  The block's idle exit
+    and relaunch are exercised too: a pause longer than its 10 ms idle timeout,
+    then more calls; then mode changes (each ends the block)."""
     import time
 
-    pc.set_zero_copy(3)
+    pc.set_zero_copy(mode)
     try:
         bad = [c["fn"] for c in kat if run_case(PcAdapter, c) != c["expect"]]
         assert not bad, bad[:5]
-        time.sleep(0.12)  # the block has exited by now
+        time.sleep(0.05)  # the block has exited by now
         small = [c for c in kat if c["fn"] != "fold"][:40]
         bad = [c["fn"] for c in small if run_case(PcAdapter, c) != c["expect"]]
         assert not bad, bad[:5]
         # switching modes ends the block; switching back restarts it
         pc.set_zero_copy(1)
-        pc.set_zero_copy(3)
+        pc.set_zero_copy(7 - mode)
+        pc.set_zero_copy(mode)
         bad = [c["fn"] for c in small if run_case(PcAdapter, c) != c["expect"]]
         assert not bad, bad[:5]
     finally:
@@ -169,18 +174,103 @@ def test_generator_reproduces_fixture_bytes(batches, name):
     assert sha(arena.cpu().numpy()) == b["arena_sha256"]
 
 
+def last_kernel() -> str:
+    buf = C.create_string_buffer(4096)
+    _lib.check("pipck_last_launch", _lib.load().pipck_last_launch(buf, len(buf)))
+    return buf.value.decode()
+
+
+# the kernel each config's bench launch runs: the fixture pins THAT kernel
+BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat<32,", 4: "k_packed<", 5: "k_flat<32,"}
+
+
 @pytest.mark.parametrize("name", sorted(ALL))
 def test_batch_kernel_reproduces_pips_results(batches, name):
+    """pip's own results (compiled pip_checksum.cpp, tests/golden/make_golden.py)
+    through the batch kernel and layout the bench runs: cfg1 at the packed 20-B
+    stride (k_small), cfg4 as a packed-lengths batch (k_packed) and, for the
+    descriptor ABI, as ragged descriptors (k_ragged)."""
     b, w = batches[name], ALL[name]
-    arena, desc, _ = _device_batch(b, w)
+    assert b["stride"] == w.stride
     pseudo = _pseudo(w)
     if w.ragged:
-        out = engine.checksum_ragged(arena, desc, pseudo)
+        arena, lens16, tc, _ = engine.gen_packed(b["n"], b["first"], b["seed"], b["hdr"])
+        outs = {"packed": engine.checksum_packed(arena, lens16, tc, b["n"], pseudo, N_FLOWS, None, b["first"])}
+        kernel = last_kernel()
+        _, desc, _ = _device_batch(b, w)
+        outs["ragged"] = engine.checksum_ragged(arena, desc, pseudo)
+        assert "k_ragged<" in last_kernel()
     else:
-        out = engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None, b["first"])
+        arena, _, _ = _device_batch(b, w)
+        outs = {"fixed": engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None,
+                                               b["first"])}
+        kernel = last_kernel()
+    assert BENCH_KERNEL[w.cfg] in kernel, kernel
+    for path, out in outs.items():
+        got = u16(out)
+        assert list(got[:16]) == b["head"], path
+        assert sha(got.astype("<u2")) == b["results_sha256"], path
+
+
+EDGES = sorted(k for k in json.loads((Path(__file__).parent / "golden" / "batches.json").read_text())
+               if k.startswith("edge_"))
+
+
+@pytest.mark.parametrize("name", EDGES)
+def test_edge_fixture_through_batch_kernel(batches, name):
+    """pip's 0x0000 / 0xFFFF corners (packets carrying their own checksum, all-zero
+    headers, an empty segment under an all-zero pseudo-header) through each
+    batch kernel the bench runs, against pip's results (make_golden.EDGES)."""
+    b = batches[name]
+    w = next(x for x in ALL.values() if x.cfg == b["cfg"])
+    n, fam = b["n"], b["family"]
+    if w.ragged:
+        arena, lens16, tc, _ = engine.gen_packed(n, b["first"], b["seed"], b["hdr"])
+    elif b["length"]:
+        arena = torch.empty(n * b["stride"], dtype=torch.uint8, device=DEV)
+        engine.gen_fixed(arena, b["stride"], b["length"], n, b["first"], b["seed"], b["hdr"])
+    else:
+        arena = torch.zeros(n * b["stride"], dtype=torch.uint8, device=DEV)
+    for o, hx in b["patches"]:
+        v = bytes.fromhex(hx)
+        arena[o:o + len(v)] = torch.frombuffer(bytearray(v), dtype=torch.uint8).to(DEV)
+    assert sha(arena.cpu().numpy()) == b["arena_sha256"]
+    pseudo = None
+    if fam:
+        flows, _ = engine.gen_flows(fam, b["n_flows"], b["seed"], b["proto"])
+        rec = 12 if fam == 4 else 36
+        if b["zero_flows"]:
+            flows.view(b["n_flows"], rec)[torch.tensor(b["zero_flows"], device=DEV), :rec - 4] = 0
+        pseudo = engine.prepare_flows(fam, flows, b["n_flows"])
+    if w.ragged:
+        out = engine.checksum_packed(arena, lens16, tc, n, pseudo, b["n_flows"], None, b["first"])
+    else:
+        out = engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None, b["first"])
+    assert b["kernel"] in last_kernel(), last_kernel()
     got = u16(out)
+    assert int((got == 0).sum()) == b["n_zero"] and int((got == 0xFFFF).sum()) == b["n_ffff"]
     assert list(got[:16]) == b["head"]
     assert sha(got.astype("<u2")) == b["results_sha256"]
+
+
+@pytest.mark.parametrize("small_k_log", [0, 1, 2, 3, 4])
+def test_small_kernel_depth_leaves_other_kernels_exact(oracle, small_k_log):
+    """Regression: the small kernel's packets-per-lane tune bits
+    (24..27) once overlapped the flat kernel's loads-only probe bit, so a valid
+    small_k_log silently broke k_flat.  Every kernel must stay exact under every
+    documented small-kernel depth."""
+    engine.tune(small_k_log=small_k_log)
+    try:
+        for w, n in ((CFG2, 300), (CFG3, 40), (CFG5, 40), (CFG1, 5000)):
+            arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+            engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
+            pseudo = _pseudo(w)
+            got = u16(engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 0))
+            host = arena.cpu().numpy()
+            want = oracle.batch_fixed(host, w.stride, w.length, n, w.family, w.proto, w.seed, N_FLOWS, 0)
+            assert np.array_equal(got, want), (w.name, small_k_log)
+    finally:
+        engine.tune()
 
 
 def test_device_flows_match_oracle(oracle):
@@ -893,15 +983,15 @@ def test_full_size_packed(oracle):
 # 9. deferred TX queue: mixed v4/v6 chains + IPv4 headers
 # ----------------------------------------------------------------------------
 @pytest.mark.parametrize("in_place", [True, False])
-def test_txq_mixed_batches_vs_oracle(oracle, in_place, monkeypatch):
+def test_txq_mixed_batches_vs_oracle(oracle, in_place):
     """in_place: small flushes read the pinned staging in place (default);
     False forces the H2D / D2H copy path that large flushes take."""
-    if not in_place:
-        monkeypatch.setenv("PIPCK_TXQ_INPLACE_MAX", "0")
     lib = _lib.load()
     ctx, q = C.c_void_p(), C.c_void_p()
     _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
     _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    if not in_place:  # per queue: every flush takes the copies
+        _lib.check("pipck_txq_inplace_max", lib.pipck_txq_inplace_max(q, 0))
     rng = np.random.default_rng(99)
     try:
         for n_pk in (1, 300, 5000):  # the queue is reused and grows
@@ -998,16 +1088,16 @@ def test_txq_submit_complete_pipeline(oracle):
 
 @pytest.mark.parametrize("in_place", [True, False])
 @pytest.mark.parametrize("register", [False, True])
-def test_txq_zero_copy_segments(oracle, register, in_place, monkeypatch):
+def test_txq_zero_copy_segments(oracle, register, in_place):
     """pipck_txq_add4_zc / add6_zc: segments read in place from pinned host
     memory (pipck_host_alloc, or a registered numpy buffer), mixed in one batch
     with staged chains and IPv4 headers; flushed and pipelined."""
-    if not in_place:
-        monkeypatch.setenv("PIPCK_TXQ_INPLACE_MAX", "0")
     lib = _lib.load()
     ctx, q = C.c_void_p(), C.c_void_p()
     _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
     _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    if not in_place:  # per queue: every flush takes the copies
+        _lib.check("pipck_txq_inplace_max", lib.pipck_txq_inplace_max(q, 0))
     rng = np.random.default_rng(4321 + register)
     size = 4 << 20
     if register:

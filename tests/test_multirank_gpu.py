@@ -21,6 +21,17 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
+def n_visible() -> int:
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def share_flag(world: int) -> list[str]:
+    """--share-gpus only where the box has fewer GPUs than ranks (bench.py refuses otherwise)."""
+    return ["--share-gpus"] if world > n_visible() else []
+
+
 def _port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -141,7 +152,8 @@ def test_bench_self_launch_cfg5_two_ranks():
     """`python bench.py --gpus 2` with no torchrun: bench.py starts both ranks
     itself (sharing the box's one GPU), each with a full cfg5 shard of 8M
     8,980-byte packets (2 x 75 GB of HBM), and rank 0 prints one JSON line."""
-    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu"]
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu",
+           *share_flag(2)]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -158,7 +170,7 @@ def test_bench_self_launch_cfg5_two_ranks():
 def test_bench_two_ranks_json_contract():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), str(ROOT / "bench.py"), "--gpus", "2",
-           "--steps", "3", "--warmup", "1", "--packets-per-gpu", "200000"]
+           "--steps", "3", "--warmup", "1", "--packets-per-gpu", "200000", *share_flag(2)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -173,10 +185,63 @@ def test_bench_two_ranks_json_contract():
 def test_bench_cfg4_two_ranks_byte_split():
     """The ragged bench under two ranks splits the global Zipf batch at equal bytes."""
     cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "cfg4", "--steps", "2",
-           "--warmup", "1", "--packets-per-gpu", "300000", "--no-cpu"]
+           "--warmup", "1", "--packets-per-gpu", "300000", "--no-cpu", *share_flag(2)]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["config"]["global_packets"] == 600000 and sum(d["per_rank_packets"]) == 600000
     assert "equal bytes" in d["config"]["parallelism"]
+
+
+def _bench_env():
+    return {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+
+
+def test_bench_four_ranks_share_flag_and_placement():
+    """an N-rank line cannot claim more GPUs than it ran on.
+    On a box with fewer than 4 GPUs, `bench.py --gpus 4` without --share-gpus
+    exits non-zero before any timed work; with the flag it runs 4 ranks, prints
+    four per-rank device records (device index + PCI bus id), says the GPUs were
+    shared, and the global packet count is the sum of the shards."""
+    if n_visible() >= 4:
+        pytest.skip("4+ GPUs visible: sharing is not needed")
+    base = [sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--steps", "2", "--warmup", "1",
+            "--packets-per-gpu", "100000", "--no-cpu"]
+    r = subprocess.run(base, capture_output=True, text=True, timeout=300, cwd=ROOT, env=_bench_env())
+    assert r.returncode != 0
+    assert "--share-gpus" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    r = subprocess.run(base + ["--share-gpus"], capture_output=True, text=True, timeout=600, cwd=ROOT,
+                       env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["distinct_gpus"] == n_visible()
+    recs = d["per_rank_device"]
+    assert [p["rank"] for p in recs] == [0, 1, 2, 3]
+    assert all(p["pci_bus_id"] and p["device"] < n_visible() for p in recs)
+    assert len({p["pci_bus_id"] for p in recs}) == n_visible()
+    assert "SHARING" in d["config"]["parallelism"]
+    assert d["per_rank_packets"] == [100000] * 4 and d["config"]["global_packets"] == sum(d["per_rank_packets"])
+
+
+def test_bench_line_names_its_kernel_and_build():
+    """The bench line names the kernel instantiation it timed (pipck_last_launch)
+    and the libpipck.so build; traffic is attached only for that exact pair."""
+    import hashlib
+
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "cfg2", "--steps", "2", "--warmup", "1",
+                        "--packets-per-gpu", "100000", "--no-cpu"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    rf = d["roofline"]
+    assert rf["kernel"].startswith("void pipck::k_flat<24, true, false, true, 4>(")
+    from pip_amd import _lib
+
+    assert rf["lib_sha256"] == hashlib.sha256(Path(_lib.LIBPIPCK).read_bytes()).hexdigest()
+    # 100000 packets is not the profiled batch: no traffic may be attached
+    assert rf["traffic"] is None and "mismatch" in rf["traffic_source"]
+    assert d["per_rank_device"][0]["pci_bus_id"]

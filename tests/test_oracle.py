@@ -3,11 +3,18 @@
 The fixtures in tests/golden/ were produced by pip's real pip_checksum.cpp
 (tests/golden/make_golden.py); these tests need no GPU and no /root/reference.
 """
+import hashlib
+import json
+from pathlib import Path
+
 import numpy as np
 import pytest
 
-from tests.golden.make_golden import run_case
+from tests.golden.make_golden import edge_inputs_cpu, oracle_edge_results, run_case
 from pip_amd.workloads import ALL, N_FLOWS
+
+EDGES = sorted(k for k in json.loads((Path(__file__).parent / "golden" / "batches.json").read_text())
+               if k.startswith("edge_"))
 
 
 def test_oracle_matches_every_known_answer(oracle, kat):
@@ -65,6 +72,37 @@ def test_generator_and_batch_match_reference_fixture(oracle, batches, name):
     assert hashlib.sha256(arena.tobytes()).hexdigest() == b["arena_sha256"]
     assert hashlib.sha256(out.astype("<u2").tobytes()).hexdigest() == b["results_sha256"]
     assert list(out[:16]) == b["head"]
+
+
+def test_fixture_layouts_are_the_shipped_ones(batches):
+    """The fixtures pin the layouts the product runs: cfg1 at the
+    packed 20-B stride the bench uses, cfg4 as the packed (16-B granular)
+    arena pipck_checksum_packed reads."""
+    assert batches["cfg1_ipv4_header"]["stride"] == ALL["cfg1_ipv4_header"].stride == 20
+    assert batches["cfg4_tcp4_zipf"]["stride"] == 0 and "lengths_sha256" in batches["cfg4_tcp4_zipf"]
+
+
+@pytest.mark.parametrize("name", EDGES)
+def test_oracle_reproduces_edge_fixture(oracle, batches, name):
+    """Edge batches (pip's 0x0000 / 0xFFFF corners through the batch layouts):
+    the CPU rebuild of the inputs matches pip's bytes and the oracle pip's results."""
+    b = batches[name]
+    arena, offs, lens, flows = edge_inputs_cpu(oracle, b)
+    assert hashlib.sha256(arena.tobytes()).hexdigest() == b["arena_sha256"]
+    out = oracle_edge_results(oracle, b, arena, offs, lens, flows)
+    assert hashlib.sha256(out.astype("<u2").tobytes()).hexdigest() == b["results_sha256"]
+    assert list(out[:16]) == b["head"]
+    assert int((out == 0).sum()) == b["n_zero"] and int((out == 0xFFFF).sum()) == b["n_ffff"]
+
+
+def test_edge_fixtures_cover_both_corners(batches):
+    edges = [batches[k] for k in EDGES]
+    assert sum(b["n_zero"] for b in edges) > 0 and sum(b["n_ffff"] for b in edges) > 0
+    # 0xFFFF under a pseudo-header (total 0: empty segment, zero addresses, proto 0)
+    assert any(b["family"] and b["n_ffff"] for b in edges)
+    # and 0x0000 through every batch kernel family the bench runs
+    kernels = {b["kernel"] for b in edges if b["n_zero"]}
+    assert {"k_flat<24,", "k_flat<32,", "k_small<", "k_packed<"} <= kernels
 
 
 def test_zipf_shape(oracle):

@@ -81,7 +81,13 @@ def main() -> None:
             med_ns = statistics.median(timed)
     except FileNotFoundError:
         timed = []
-    traffic = {"workload": wl, "tag": tag, "kernel": kname, "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+    bench_kernel = bench["roofline"].get("kernel")
+    if bench_kernel != kname:
+        print(f"WARNING: rocprof's dominant kernel {kname!r} is not the one the bench line timed "
+              f"({bench_kernel!r}); bench.py will not attach this traffic", file=sys.stderr)
+    traffic = {"workload": wl, "tag": tag, "kernel": kname, "lib_sha256": bench["roofline"].get("lib_sha256"),
+               "bench_kernel_matches": bench_kernel == kname,
+               "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
                "hbm_bytes_per_launch": int(hbm), "algorithmic_bytes_per_launch": algo,
                "arena_stride": bench["config"]["arena_stride"], "packets": bench["config"]["packets_per_gpu"],
                "traffic_over_algorithmic": round(hbm / algo, 4), "rocprof_avg_ns": avg_ns,
@@ -101,7 +107,9 @@ def main() -> None:
     for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:6]:
         md.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                   f"{float(r['Percentage']):.2f}% |")
-    md += ["", f"Dominant kernel: `{kname[:120]}`", "",
+    md += ["", f"Dominant kernel: `{kname}`", "",
+           f"* libpipck.so sha256 `{bench['roofline'].get('lib_sha256')}` (bench.py attaches this traffic "
+           f"only to lines of this kernel and build)",
            f"* rocprof kernel trace, the {len(timed)} timed dispatches: mean {avg_ns / 1e6:.4f} ms, median "
            f"{(med_ns if timed else avg_ns) / 1e6:.4f} ms; --stats average over all {top['Calls']} calls (warm-up "
            f"included) {all_ns / 1e6:.4f} ms",
