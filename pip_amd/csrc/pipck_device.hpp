@@ -123,4 +123,18 @@ __device__ __forceinline__ u32x4 buf_load(buf_t r, uint32_t off) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT ? 2 : 0);  // aux bit 1 = nt (gfx94x/950)
 }
 
+// Result stores (2 B per packet, 1 B for RX verify) with the system-coherent
+// policy (sc1): written through rather than left dirty in L2.  Plain stores of
+// the results cost the flat kernel 2.7-4.5 % of cfg2's time -- dirty result
+// lines evicted in the middle of the read stream -- and sc1 stores of the
+// same results cost nothing measurable (tools/probe/write_probe.hip,
+// profiles/r03_write_probe.jsonl).  Range-checked like the loads.
+constexpr int kStoreSc1 = 16;  // gfx940+ cache-policy bit SC1
+__device__ __forceinline__ void store_result16(buf_t r, uint32_t byte_off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, (int)byte_off, 0, kStoreSc1);
+}
+__device__ __forceinline__ void store_result8(buf_t r, uint32_t byte_off, uint32_t v) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, (int)byte_off, 0, kStoreSc1);
+}
+
 }  // namespace pipck

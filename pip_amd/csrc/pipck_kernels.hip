@@ -70,6 +70,11 @@ __global__ void k_flows6(const pipck_flow6* __restrict__ f, uint32_t n, uint32_t
     pseudo[i] = s + f[i].proto;
 }
 
+// tune flags bit 29 (same results): result stores with the r02 policies
+// (plain write-back stores in k_flat / k_packed, non-temporal in k_small)
+// instead of the write-through sc1 stores (store_result16)
+constexpr uint32_t kPlainResultStores = 1u << 29;
+
 // ---------------------------------------------------------------------------
 // fixed-stride kernel
 // ---------------------------------------------------------------------------
@@ -149,7 +154,7 @@ template <int NL, int K, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
                                                uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
     const int lane = threadIdx.x & 63;
     const uint64_t base = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64u * K);
     if (base >= n) return;  // wave-uniform
@@ -196,14 +201,28 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena
         const uint32_t F = be_fold(fold64(acc), addr);
         res[k] = VERIFY ? (uint32_t)(fold16(P[k] + lterm + F) == 0xFFFFu) : (uint32_t)finish(P[k] + lterm, F);
     }
+    // result stores: write-through (sc1, see store_result16) by default; tune
+    // flags bit 29 = the r02 non-temporal stores
+    const uint32_t nv = (uint32_t)min<uint64_t>(64u * K, n - base);
+    if (kflags & kPlainResultStores) {
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint64_t pkt = base + 64u * k + lane;
-        if (pkt < n) {
+        for (int k = 0; k < K; k++) {
+            const uint64_t pkt = base + 64u * k + lane;
+            if (pkt < n) {
+                if (VERIFY)
+                    __builtin_nontemporal_store((uint8_t)res[k], &ok[pkt]);
+                else
+                    __builtin_nontemporal_store((uint16_t)res[k], &out[pkt]);
+            }
+        }
+    } else {
+        const buf_t rb = VERIFY ? buf_rsrc(ok + base, nv) : buf_rsrc(out + base, 2u * nv);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
             if (VERIFY)
-                __builtin_nontemporal_store((uint8_t)res[k], &ok[pkt]);
+                store_result8(rb, 64u * k + lane, res[k]);
             else
-                __builtin_nontemporal_store((uint16_t)res[k], &out[pkt]);
+                store_result16(rb, 2u * (64u * k + lane), res[k]);
         }
     }
 }
@@ -331,6 +350,25 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v) {
 // on gfx9 both count in VM_CNT, so inside the row loop each one would make the
 // next row's wait drain every load in flight.
 constexpr uint32_t kFlatMaxRun = 64;  // packets per wave task
+// tune flags bit 21 (MEASUREMENT ONLY, wrong results): the flat kernel's
+// rows are waited for and consumed by one add each, with no per-packet
+// work, so tools can time the access pattern alone.  (Bits 24..27 are the
+// small kernel's packets per lane: this bit must not overlap them.)
+constexpr uint32_t kLoadsOnly = 1u << 21;
+// tune flags bit 22 (MEASUREMENT ONLY, no results): k_flat skips its task end
+// (the per-packet LDS sums, pseudo-header add and result stores)
+constexpr uint32_t kNoTaskEnd = 1u << 22;
+// bit 23: k_flat's task end computes every result but stores none;
+// bit 28: every task stores its results into the batch's FIRST 64 slots (one
+// 128-B line shared by all waves; both MEASUREMENT ONLY, wrong results)
+constexpr uint32_t kEndNoStore = 1u << 23;
+constexpr uint32_t kEndSameLine = 1u << 28;
+// EXPERIMENTAL (same results): bit 30 = per-wave result stores (the r02 scheme) instead of one coalesced
+// store of the whole block's results by its last wave; bit 31 = wave tasks of
+// exactly the packet count the heuristic names, not rounded to a multiple of 16
+
+constexpr uint32_t kFlatWaveStores = 1u << 30;
+constexpr uint32_t kFlatFreeRun = 1u << 31;
 // u16 slots per lane row: >= run, and an odd number of dwords so the 64 lanes
 // of one ds_write_b16 land in distinct banks (mod 32)
 __host__ __device__ constexpr uint32_t flat_pitch(uint32_t run) {
@@ -359,21 +397,31 @@ __device__ __forceinline__ uint32_t flat_pseudo(uint64_t p0, uint32_t np, const 
     return pseudo[(flow_origin + p0 + 64u) >> 32 ? (uint32_t)(f % n_flows) : (uint32_t)f % n_flows];
 }
 
-template <bool VERIFY>
+template <bool VERIFY, bool TO_LDS = false>
 __device__ __forceinline__ void flat_write(const uint16_t* part, uint32_t pitch, uint64_t p0, uint32_t np,
                                            uint32_t Pb, bool has_pseudo, uint32_t lterm, uint16_t* out, uint8_t* ok,
-                                           int lane) {
+                                           int lane, uint32_t kflags, uint64_t magic) {
     if ((uint32_t)lane >= np) return;
     uint32_t s = 0;
 #pragma unroll 16
     for (int j = 0; j < 64; j++) s += part[j * pitch + lane];
     const uint32_t F = bswap16(fold16(s));  // packets start 16-byte aligned: even address
     const uint32_t P = has_pseudo ? Pb + lterm : 0u;
-    const uint64_t pkt = p0 + lane;
-    if (VERIFY)
-        ok[pkt] = fold16(P + F) == 0xFFFFu;
-    else
-        out[pkt] = finish(P, F);
+    const uint64_t pkt = (kflags & kEndSameLine) ? (uint64_t)lane : p0 + lane;
+    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    if (!TO_LDS && (kflags & kEndNoStore) && (uint64_t)r != magic) return;  // measurement: never stores
+    if (TO_LDS) {
+        out[lane] = (uint16_t)r;  // `out` is this wave's row of the block's LDS results
+    } else if (kflags & kPlainResultStores) {
+        if (VERIFY)
+            ok[pkt] = (uint8_t)r;
+        else
+            out[pkt] = (uint16_t)r;
+    } else if (VERIFY) {
+        store_result8(buf_rsrc(ok + p0, np), (uint32_t)(pkt - p0), r);
+    } else {
+        store_result16(buf_rsrc(out + p0, 2u * np), 2u * (uint32_t)(pkt - p0), r);
+    }
 }
 
 // Row bookkeeping is incremental (cpp >= 64, so a row advances the packet by at
@@ -414,11 +462,6 @@ __device__ __forceinline__ void flat_load_rows(u32x4 (&v)[U], buf_t tb, uint32_t
     for (int u = 0; u < U; u++) flat_load_row<NT>(v[u], tb, r0 + u * 64, lp, cpp, nch, lane);
 }
 
-// tune flags bit 21 (MEASUREMENT ONLY, wrong results): the flat kernel's
-// rows are waited for and consumed by one add each, with no per-packet
-// work, so tools can time the access pattern alone.  (Bits 24..27 are the
-// small kernel's packets per lane: this bit must not overlap them.)
-constexpr uint32_t kLoadsOnly = 1u << 21;
 
 // rs < tchunks (wave-uniform)
 __device__ __forceinline__ void flat_reduce_row(const u32x4& v, uint32_t rs, uint32_t tchunks, const RowPos& pp,
@@ -482,6 +525,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
     const uint64_t n_tasks = (n + run - 1) / run;
     const TaskRange tr = xcd_tasks<WPB>(n_tasks, (kflags & kXcdGroups) != 0);
     const TraceBuf trb = trace_buf(kflags);
+    // Block-coalesced result stores (the default; needs one task per wave and
+    // the block's waves on consecutive tasks): each wave parks its packets'
+    // results in LDS and the block's LAST wave to finish writes all of them
+    // with one coalesced store per 64 results.  Scattered per-wave stores of
+    // 2 * run bytes hit partial 128-B lines that HBM3E (no write mask) must
+    // read-modify-write between the read streams: they cost cfg2 4.5 % and
+    // cfg5 1.5 % -- as much as the whole task end -- while the same stores all
+    // aimed at one line cost nothing (profiles/r03_flat_end_probe.jsonl).  With
+    // run a multiple of 16 (launch_fixed) a block's results are whole lines.
+    const bool coalesce = !(kflags & (kFlatWaveStores | kXcdGroups | kEndSameLine)) && (uint64_t)gridDim.x * WPB >= n_tasks;
+    uint16_t* bres = s_part + WPB * 64u * pitch;                       // WPB * run u16
+    uint32_t* bcnt = reinterpret_cast<uint32_t*>(bres + ((WPB * run + 1u) & ~1u));
+    if (coalesce) {
+        if (threadIdx.x == 0) *bcnt = 0;
+        __syncthreads();
+    }
     for (uint64_t task = tr.first; task < tr.end; task += tr.step) {
         const uint64_t t_start = (kflags & kTrace) ? trace_clock() : 0;
         const uint64_t p0 = task * run;
@@ -537,7 +596,42 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
         }
         flat_stash(acc, np - 1, part, pitch, lane);
         wave_sync();
-        flat_write<VERIFY>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane);
+        if (coalesce && !(kflags & kNoTaskEnd)) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+            flat_write<VERIFY, true>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, bres + w * run, ok, lane,
+                                     kflags, flow_origin | 0xFFFF000000000000ull);
+            // release this wave's results, count it in; the last of the block's
+            // active waves sees every other wave's results (LDS ops of a wave
+            // complete in order; the fences order them against the count)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            uint32_t prev = 0;
+            if (lane == 0) prev = atomicAdd(bcnt, 1u);
+            prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
+            const uint64_t t0 = (uint64_t)blockIdx.x * WPB;
+            const uint32_t active = (uint32_t)min<uint64_t>(WPB, n_tasks - t0);
+            if (prev + 1 == active) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const uint64_t q0 = t0 * run;
+                const uint32_t cnt = (uint32_t)min<uint64_t>((uint64_t)WPB * run, n - q0);
+                if (kflags & kPlainResultStores) {
+                    for (uint32_t i = lane; i < cnt; i += 64) {
+                        if (VERIFY)
+                            ok[q0 + i] = (uint8_t)bres[i];
+                        else
+                            out[q0 + i] = bres[i];
+                    }
+                } else if (VERIFY) {
+                    const buf_t rb = buf_rsrc(ok + q0, cnt);
+                    for (uint32_t i = lane; i < cnt; i += 64) store_result8(rb, i, bres[i]);
+                } else {
+                    const buf_t rb = buf_rsrc(out + q0, 2u * cnt);
+                    for (uint32_t i = lane; i < cnt; i += 64) store_result16(rb, 2u * i, bres[i]);
+                }
+            }
+        } else if (!(kflags & kNoTaskEnd)) {
+            flat_write<VERIFY>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane, kflags,
+                               flow_origin | 0xFFFF000000000000ull);
+        }
         trace_task(kflags, trb, task, t_start, lane);
         wave_sync();
     }
@@ -1192,13 +1286,21 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
     // MARKS: the marks path compiled alone (the scalar end loop folded away)
     const uint32_t le_sum =
         ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len, nch, true, MARKS ? kflags | kPackedMarksOnly : kflags);
-    if (valid) {
-        const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
-        const uint32_t P = pseudo ? Pbase + len : 0u;
-        if (VERIFY)
-            ok[seg] = fold16(P + F) == 0xFFFFu;
-        else
-            out[seg] = finish(P, F);
+    const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
+    const uint32_t P = pseudo ? Pbase + len : 0u;
+    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
+    if (kflags & kPlainResultStores) {
+        if (valid) {
+            if (VERIFY)
+                ok[seg] = (uint8_t)r;
+            else
+                out[seg] = (uint16_t)r;
+        }
+    } else if (VERIFY) {  // write-through (sc1): see store_result16; lanes past the batch are range-checked off
+        store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, r);
+    } else {
+        store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, r);
     }
     trace_task(kflags, trb, tile, t_start, lane);
 }
@@ -1325,9 +1427,11 @@ static const Variant& pick_variant(uint32_t nch) {
 }
 
 constexpr uint32_t kNoSmall = 64u;  // pipck_tune flags bit 6: never the small-packet kernel
+typedef void (*small_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
+                         uint64_t, uint16_t*, uint8_t*, uint32_t);
 struct SmallVariant {
     int k;              // packets per lane per wave task
-    fixed_fn fn[4][2][2];  // [nl-1][verify][nt]
+    small_fn fn[4][2][2];  // [nl-1][verify][nt]
 };
 #define PIPCK_S1(NL, K)                                                                            \
     {                                                                                              \
@@ -1456,11 +1560,19 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t flags = g_tune.flags.load();
         const uint32_t loads = g_tune.loads.load() ? g_tune.loads.load() : (jumbo ? 33u : 25u);
         const FlatVariant* fv = &flat_variant(loads);
-        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 128u : 64u);
-        const uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
+        const uint32_t rows = (flags >> 8) & 0xFFu ? (flags >> 8) & 0xFFu : (jumbo ? 96u : 46u);
+        uint32_t run = std::min(kFlatMaxRun, std::max<uint32_t>(1u, (64u * rows) / cpp));
+        // Shorter packets: a multiple of 16 packets per wave task, so a block's
+        // results (4 * run u16) are whole 128-B lines (written once, by the
+        // block's last wave, see k_flat).  Measured with the sc1 result stores
+        // (profiles/r03_flat_rows_scan.jsonl): cfg2 runs 0.884 ms at 32 packets
+        // per task (46.5 rows) against 0.906 at 31 and 0.906 at 48; jumbo
+        // packets are best at ~10 packets (96 rows), unrounded.
+        if (!(flags & kFlatFreeRun) && !jumbo && run >= 12) run = std::min(kFlatMaxRun, (run + 8) / 16 * 16);
         const uint64_t tasks = (n + run - 1) / run;
         const uint32_t grid = grid_for(4, tasks, 0);
-        const size_t lds = 4u * 64u * flat_pitch(run) * sizeof(uint16_t);
+        // per-wave partials + the block's results + its completion counter
+        const size_t lds = (4u * 64u * flat_pitch(run) + ((4u * run + 1u) & ~1u)) * sizeof(uint16_t) + 16u;
         PIPCK_LAUNCH(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
@@ -1520,7 +1632,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint64_t waves = (n + 64u * sv.k - 1) / (64u * sv.k);
         PIPCK_LAUNCH(sv.fn[small_nl ? small_nl - 1 : 0][verify][nt_for(false)], dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0,
                            as_stream(stream), (const uint8_t*)d_arena, stride, len, n, d_pseudo,
-                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
+                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, g_tune.flags.load());
         PIPCK_LAUNCHED("k_small");
         return PIPCK_OK;
     }
