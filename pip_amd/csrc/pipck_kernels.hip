@@ -70,9 +70,9 @@ __global__ void k_flows6(const pipck_flow6* __restrict__ f, uint32_t n, uint32_t
     pseudo[i] = s + f[i].proto;
 }
 
-// tune flags bit 29 (same results): result stores with the r02 policies
-// (plain write-back stores in k_flat / k_packed, non-temporal in k_small)
-// instead of the write-through sc1 stores (store_result16)
+// tune flags bit 29 (same results): k_flat / k_packed store their results
+// with plain write-back stores (the r02 policy) instead of the write-through
+// sc1 stores (store_result16)
 constexpr uint32_t kPlainResultStores = 1u << 29;
 
 // ---------------------------------------------------------------------------
@@ -201,30 +201,21 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena
         const uint32_t F = be_fold(fold64(acc), addr);
         res[k] = VERIFY ? (uint32_t)(fold16(P[k] + lterm + F) == 0xFFFFu) : (uint32_t)finish(P[k] + lterm, F);
     }
-    // result stores: write-through (sc1, see store_result16) by default; tune
-    // flags bit 29 = the r02 non-temporal stores
-    const uint32_t nv = (uint32_t)min<uint64_t>(64u * K, n - base);
-    if (kflags & kPlainResultStores) {
+    // Non-temporal result stores.  Results are 2 B per 20-B header here (10 %
+    // of the bytes, unlike the streaming kernels' 0.1 %): the write-through sc1
+    // policy that the streaming kernels use measured 0.5-1 % slower at 64M-256M
+    // headers (profiles/r03_sc1_stores_scan.jsonl), so k_small keeps nt.
 #pragma unroll
-        for (int k = 0; k < K; k++) {
-            const uint64_t pkt = base + 64u * k + lane;
-            if (pkt < n) {
-                if (VERIFY)
-                    __builtin_nontemporal_store((uint8_t)res[k], &ok[pkt]);
-                else
-                    __builtin_nontemporal_store((uint16_t)res[k], &out[pkt]);
-            }
-        }
-    } else {
-        const buf_t rb = VERIFY ? buf_rsrc(ok + base, nv) : buf_rsrc(out + base, 2u * nv);
-#pragma unroll
-        for (int k = 0; k < K; k++) {
+    for (int k = 0; k < K; k++) {
+        const uint64_t pkt = base + 64u * k + lane;
+        if (pkt < n) {
             if (VERIFY)
-                store_result8(rb, 64u * k + lane, res[k]);
+                __builtin_nontemporal_store((uint8_t)res[k], &ok[pkt]);
             else
-                store_result16(rb, 2u * (64u * k + lane), res[k]);
+                __builtin_nontemporal_store((uint16_t)res[k], &out[pkt]);
         }
     }
+    (void)kflags;
 }
 
 // ---------------------------------------------------------------------------
