@@ -2,8 +2,8 @@
 // functions (pip/pip_checksum.h:17-34, plus pip_fold_uint32 at
 // pip/pip_checksum.cpp:9) with identical signatures, computed on the MI355X.
 //
-// Each call marshals its pseudo-header terms (pip_checksum.cpp:46-55, 70-82,
-// 130-142, 161-176) into the initial sum and hands the payload bytes -- one
+// Each call marshals its pseudo-header terms (pip_checksum.cpp:45-55, 66-82,
+// 92-107, 120-142) into the initial sum and hands the payload bytes -- one
 // segment, or every segment of a pip_buf chain in order -- to
 // pipck_host_sum(), which replays pip's per-segment loop on the device.
 // Contexts are per thread (thread_local), so calls stay reentrant and

@@ -360,6 +360,9 @@ constexpr uint32_t kEndSameLine = 1u << 28;
 
 constexpr uint32_t kFlatWaveStores = 1u << 30;
 constexpr uint32_t kFlatFreeRun = 1u << 31;
+// bit 30 in k_packed: tile rows on the r02 grid (from the tile's first chunk)
+// instead of the 128-B line grid
+constexpr uint32_t kPackedNoAlign = 1u << 30;
 // u16 slots per lane row: >= run, and an odd number of dwords so the 64 lanes
 // of one ds_write_b16 land in distinct banks (mod 32)
 __host__ __device__ constexpr uint32_t flat_pitch(uint32_t run) {
@@ -1032,7 +1035,7 @@ constexpr uint32_t kPackedMarksOnly = 1u << 19;  // pipck_tune flags bit 19: mix
 __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint32_t row, uint32_t total, int lane,
                                                          const u32x4& v, uint32_t pre_v, uint32_t endt_v,
                                                          uint32_t& s0, uint32_t& e0, uint32_t& racc, uint32_t& rseg,
-                                                         uint32_t kflags) {
+                                                         uint32_t kflags, uint32_t lead) {
     if (row >= e0) {  // wave-uniform: the row starts past segment s0
         s0 = (uint32_t)__popcll(__ballot(pre_v <= row)) - 1u;
         e0 = (uint32_t)__builtin_amdgcn_readlane((int)endt_v, (int)s0) & 0xFFFFFFu;
@@ -1040,7 +1043,10 @@ __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint3
     s0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
     e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e0);
     rseg = (uint32_t)__builtin_amdgcn_readfirstlane((int)rseg);  // keep the run state scalar
-    if (e0 > row + 64) {  // interior row: all 64 chunks are whole chunks of s0 (and < total)
+    // interior row: all 64 chunks are whole chunks of s0 (and < total); the
+    // first row of a tile with lead chunks (the previous tile's bytes before
+    // the line-aligned start, see k_packed) takes the masked path
+    if (e0 > row + 64 && (row != 0 || lead == 0)) {
         if (s0 != rseg) {
             ragged_flush(t, lane, racc, rseg);
             rseg = s0;
@@ -1061,7 +1067,7 @@ __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint3
         rseg = kNoSeg;
     }
     const uint32_t c = row + lane;
-    const bool active = c < total;
+    const bool active = c < total && c >= lead;
     const uint32_t end_v = endt_v & 0xFFFFFFu;
     const uint32_t k = (uint32_t)__popcll(__ballot(end_v > row && end_v <= row + 64));  // ends s0 .. s0+k-1
     uint32_t s;
@@ -1110,7 +1116,7 @@ __device__ __forceinline__ void ragged_reduce_row_packed(RaggedTileLds& t, uint3
 template <int U, bool PIPE, bool NT, bool PACKED>
 __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, int lane, uintptr_t tbase,
                                               uint32_t pre_v, uint32_t endt_v, uint32_t& racc, uint32_t& rseg,
-                                              uint32_t kflags) {
+                                              uint32_t kflags, uint32_t lead) {
     u32x4 v[U];
     uint32_t sx[U];
     uint32_t scur = 0;
@@ -1125,7 +1131,8 @@ __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, 
             const uint32_t row = c0 + u * 64;
             if (row < total) {  // wave-uniform
                 if (PACKED)
-                    ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, endt_v, s0, e0, racc, rseg, kflags);
+                    ragged_reduce_row_packed(t, row, total, lane, v[u], pre_v, endt_v, s0, e0, racc, rseg, kflags,
+                                             lead);
                 else
                     ragged_reduce_row(t, row, total, lane, v[u], sx[u], racc, rseg);
             }
@@ -1146,7 +1153,8 @@ __device__ __forceinline__ void ragged_stream(RaggedTileLds& t, uint32_t total, 
 // segment's base; others map chunks to segments through the LDS prefix.
 template <int U, bool PIPE, bool NT>
 __device__ __forceinline__ uint32_t ragged_tile_sum(RaggedTileLds& t, int lane, uintptr_t addr, uint32_t head,
-                                                    uint32_t len, uint32_t nch, bool packed_hint, uint32_t kflags) {
+                                                    uint32_t len, uint32_t nch, bool packed_hint, uint32_t kflags,
+                                                    uint32_t lead = 0) {
     if (__all(nch <= kTinyChunks) && !(kflags & kNoTinyTiles)) {
         // Tiny-segment tile (IPv4 headers, bare TCP/UDP headers): every lane
         // sums its own segment with its loads all in flight; no chunk stream.
@@ -1181,9 +1189,10 @@ __device__ __forceinline__ uint32_t ragged_tile_sum(RaggedTileLds& t, int lane, 
     uint32_t rseg = kNoSeg;
     if (packed)
         ragged_stream<U, PIPE, NT, true>(t, total, lane, tbase, incl - nch, incl | (len & 15u) << 24, racc, rseg,
-                                         kflags);
+                                         kflags, lead);
     else  // fewer rows in flight: the lookup path needs a segment register per row
-        ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg, kflags);
+        ragged_stream<(U < 4 ? U : 4), PIPE, NT, false>(t, total, lane, tbase, incl - nch, incl, racc, rseg, kflags,
+                                                        0u);
     ragged_flush(t, lane, racc, rseg);
     wave_sync();
     return t.acc[lane];
@@ -1271,12 +1280,20 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
         const uint32_t f0 = (uint32_t)((flow_origin + tile * 64) % n_flows);  // one 64-bit modulo per tile
         Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
     }
+    // The tile's row grid starts on the 128-B line holding its first byte: the
+    // `lead` chunks before it (the previous tile's last bytes) are loaded and
+    // zeroed, and packet 0 of the tile is streamed as if it began there, so
+    // every 1 KiB row is 8 whole lines and no line is fetched by two rows of a
+    // tile (tune flags bit 30: the r02 grid from the tile's first chunk).
+    const uintptr_t tbase = (uintptr_t)arena + 16ull * tile_chunk[tile];
     const uint32_t nch = (len + 15) >> 4;
-    const uint32_t excl = wave_incl_scan(nch) - nch;
-    const uintptr_t addr = (uintptr_t)arena + 16ull * (tile_chunk[tile] + excl);
+    const uint32_t lead = (__all(nch <= kTinyChunks) || (kflags & kPackedNoAlign)) ? 0u : (uint32_t)(tbase >> 4) & 7u;
+    const uint32_t nch_s = nch + (lane == 0 ? lead : 0u);
+    const uint32_t excl = wave_incl_scan(nch_s) - nch_s;
+    const uintptr_t addr = tbase - 16u * lead + 16ull * excl;
     // MARKS: the marks path compiled alone (the scalar end loop folded away)
-    const uint32_t le_sum =
-        ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len, nch, true, MARKS ? kflags | kPackedMarksOnly : kflags);
+    const uint32_t le_sum = ragged_tile_sum<U, true, NT>(t, lane, addr, 0u, len + (lane == 0 ? 16u * lead : 0u), nch_s,
+                                                         true, MARKS ? kflags | kPackedMarksOnly : kflags, lead);
     const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
     const uint32_t P = pseudo ? Pbase + len : 0u;
     const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);

@@ -91,7 +91,7 @@ def main():
                         assert torch.equal(out, ref)
             for xcd, ms in res.items():
                 m = statistics.median(ms)
-                print(json.dumps({"workload": w.name, "packets": n, "gbytes": round(nbytes / 1e9, 1),
+                print(json.dumps({"workload": w.name, "packets": n, "gbytes": round(nbytes / 1e9, 1), "bytes": nbytes,
                                   "arm": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}),
                       flush=True)
             engine.tune()
