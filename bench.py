@@ -176,13 +176,13 @@ def run_rank(args) -> int:
             del lens_all, prefix
         else:
             first, count, lens = 0, n_total, None
-        # the packed layout: packets back to back at 16-byte granularity, u16
-        # lengths + one u64 per 64 packets instead of 16-byte descriptors
-        arena, lens16, tile_chunk, lens = engine.gen_packed(count, first, w.seed, w.hdr, lengths=lens)
+        # the byte-packed layout: packets back to back with no padding, u16
+        # lengths + one u64 byte offset per 64 packets instead of 16-byte descriptors
+        arena, lens16, tile_off, lens = engine.gen_packed_bytes(count, first, w.seed, w.hdr, lengths=lens)
         l4_bytes = int(lens.to(torch.int64).sum().item())
 
         def step(out):
-            return engine.checksum_packed(arena, lens16, tile_chunk, count, pseudo, N_FLOWS, None, first, out=out)
+            return engine.checksum_packed_bytes(arena, lens16, tile_off, count, pseudo, N_FLOWS, None, first, out=out)
     else:
         first, count = shard.shard_range(n_total, env.world, env.rank)
         arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
@@ -261,6 +261,8 @@ def run_rank(args) -> int:
             "global_packets": int(total_pkts),
             "l4_bytes_per_packet": w.length,
             "arena_stride": w.stride,
+            "layout": "byte-packed (no padding), u16 lengths + u64 byte offset per 64 packets" if w.ragged
+                      else f"fixed {w.stride}-byte slots",
             "parallelism": f"{env.world} shard(s), contiguous packet ranges"
                            f"{' of equal bytes' if w.ragged else ''}, no data-path collective"
                            f"{f', {env.world} ranks SHARING {env.world - n_shared} GPU(s) (--share-gpus)' if n_shared else ''}",

@@ -122,6 +122,25 @@ int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint6
  * chunks) from the lengths, on the stream. */
 int pipck_packed_index(const uint16_t* d_lens, uint64_t n_packets, uint64_t* d_tile_chunk, void* stream);
 
+/* Byte-packed ragged batch: packets back to back with NO padding -- packet i
+ * at d_arena + b_i, b_i = len_0 + ... + len_{i-1} (a capture buffer, a
+ * socket ring read in order, cfg4's bench layout).  d_tile_off[t] = b_{64 t}
+ * for t = 0 .. ceil(n/64) (the last entry = the batch's bytes;
+ * pipck_packed_bytes_index builds it), so the kernel reads 2 + 1/8 bytes of
+ * metadata per packet and nothing but packet bytes otherwise (the 16-byte
+ * granular layout above reads its padding too: 0.76 % of cfg4's bytes).
+ * d_arena must be 128-byte aligned and readable up to the 16-byte boundary
+ * after the last packet (any hipMalloc'd buffer of the batch's size is).
+ * Flows and results as pipck_checksum_packed (pip_inet{,6}_checksum,
+ * pip_checksum.cpp:42-87); any lengths 0..65535. */
+int pipck_checksum_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off,
+                                uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows,
+                                const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, void* stream);
+int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off,
+                              uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows,
+                              const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok, void* stream);
+int pipck_packed_bytes_index(const uint16_t* d_lens, uint64_t n_packets, uint64_t* d_tile_off, void* stream);
+
 /* Chains (pip_buf lists, pip_checksum.cpp:90-148): packet p owns segments
  * [d_seg_begin[p], d_seg_begin[p+1]); its pseudo-header length term is the
  * u32 sum of its segment lengths (pip_buf::total_len).  Every segment is
@@ -182,6 +201,9 @@ int pipck_gen_ragged_layout(const uint32_t* d_len, uint64_t n, uint64_t first_pk
                             pipck_desc* d_desc, uint64_t* arena_bytes, void* stream);
 int pipck_gen_ragged_fill(void* d_arena, const pipck_desc* d_desc, uint64_t n, uint64_t first_pkt,
                           uint64_t seed, uint32_t hdr_kind, void* stream);
+/* byte-packed layout (pipck_checksum_packed_bytes): packets [first_pkt, first_pkt+n) with lengths d_lens */
+int pipck_gen_packed_bytes(void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
+                           uint64_t first_pkt, uint64_t seed, uint32_t hdr_kind, void* stream);
 int pipck_gen_flows4(pipck_flow4* d_flows, uint32_t n_flows, uint64_t seed, uint8_t proto, void* stream);
 int pipck_gen_flows6(pipck_flow6* d_flows, uint32_t n_flows, uint64_t seed, uint8_t proto, void* stream);
 

@@ -180,6 +180,23 @@ class Oracle(_Common):
         self.lib.ock_gen_ragged_fill(seed, first, n, hdr, _np_ptr(lens), _np_ptr(offs), _np_ptr(arena), threads)
         return arena, offs[:n], lens[:n]
 
+    def gen_packed_bytes_batch(self, seed: int, first: int, n: int, hdr: int):
+        """Zipf batch in the byte-packed layout (no padding between packets): (arena, offsets, lens).
+        Same packet bytes as gen_ragged_batch; packets filled in order on one thread, so each packet's
+        16-byte-rounded zero tail is overwritten by the next packet."""
+        lens = np.zeros(max(n, 1), dtype=np.uint32)
+        offs16 = np.zeros(max(n, 1), dtype=np.uint64)
+        self.lib.ock_gen_ragged_layout(seed, first, n, _np_ptr(lens), _np_ptr(offs16))
+        lens = lens[:n]
+        offs = np.zeros(max(n, 1), dtype=np.uint64)
+        if n:
+            offs[1:n] = np.cumsum(lens[:-1], dtype=np.uint64)
+        total = int(offs[n - 1] + lens[n - 1]) if n else 0
+        arena = np.zeros(total + 32, dtype=np.uint8)
+        self.lib.ock_gen_ragged_fill(seed, first, n, hdr, _np_ptr(lens), _np_ptr(offs), _np_ptr(arena), 1)
+        arena[total:] = 0
+        return arena[:(total + 15) // 16 * 16], offs[:n], lens
+
     # ---- batch checksums
     def batch_fixed(self, arena: np.ndarray, stride: int, length: int, n: int, family: int, proto: int,
                     seed: int, n_flows: int, flow_origin: int = 0, threads: int = 1) -> np.ndarray:

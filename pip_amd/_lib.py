@@ -53,6 +53,10 @@ SIGNATURES = {
     "pipck_checksum_packed": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_verify_packed": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_packed_index": (_i32, [_p, _u64, _p, _p]),
+    "pipck_checksum_packed_bytes": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
+    "pipck_verify_packed_bytes": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
+    "pipck_packed_bytes_index": (_i32, [_p, _u64, _p, _p]),
+    "pipck_gen_packed_bytes": (_i32, [_p, _p, _p, _u64, _u64, _u64, _u32, _p]),
     "pipck_checksum_chains": (_i32, [_p, _p, _u64, _p, _p, _u64, _p, _p, _p, _p, _p]),
     "pipck_verify_fixed": (_i32, [_p, _u64, _u32, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_verify_ragged": (_i32, [_p, _p, _u64, _p, _p, _p, _p]),

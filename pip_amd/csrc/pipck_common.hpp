@@ -35,6 +35,17 @@ inline int hip_fail(hipError_t e, const char* what) {
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The batch kernel this thread launched last (its host-side handle), so a
+// measurement can name the exact template instantiation it timed
+// (pipck_last_launch in pipck_testing.h: bench.py binds a PMC traffic file to
+// that name).  One thread-local store per launch.
+extern thread_local const void* t_last_kernel;
+#define PIPCK_LAUNCH(K, ...)                                          \
+    do {                                                              \
+        ::pipck::t_last_kernel = reinterpret_cast<const void*>(K);    \
+        hipLaunchKernelGGL(K, __VA_ARGS__);                           \
+    } while (0)
+
 // Number of CUs on the current device (cached per device).
 int device_cus();
 

@@ -128,6 +128,26 @@ __global__ __launch_bounds__(256) void k_gen_ragged(uint8_t* __restrict__ arena,
     }
 }
 
+// Byte-packed batch (pipck_checksum_packed_bytes' layout): packet i (global id
+// first + i) at tile_off[i / 64] + the lengths before it in its tile, no
+// padding.  One wave per tile; lanes write a packet's bytes, packet by packet.
+__global__ __launch_bounds__(64) void k_gen_packedb(uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
+                                                    const uint64_t* __restrict__ tile_off, uint64_t n, uint64_t first,
+                                                    uint64_t seed, uint32_t hdr) {
+    const int lane = threadIdx.x;
+    const uint64_t t = blockIdx.x;
+    uint64_t off = tile_off[t];
+    for (uint32_t k = 0; k < 64 && t * 64 + k < n; k++) {
+        const uint64_t i = t * 64 + k;
+        const uint32_t len = lens[i];
+        const uint64_t key = pkt_key(seed, first + i);
+        const uint32_t cls = packet_class(key);
+        for (uint32_t b = lane; b < len; b += 64)
+            arena[off + b] = (uint8_t)(packet_word(key, cls, len, hdr, b / 8) >> (8 * (b % 8)));
+        off += len;
+    }
+}
+
 __global__ void k_gen_flows(uint8_t* __restrict__ out, uint32_t n, uint64_t seed, uint8_t proto, int v6) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -260,6 +280,19 @@ int pipck_gen_ragged_fill(void* d_arena, const pipck_desc* d_desc, uint64_t n, u
     hipLaunchKernelGGL(k_gen_ragged, dim3(gen_grid(n)), dim3(256), 0, as_stream(stream), (uint8_t*)d_arena, d_desc, n,
                        first_pkt, seed, hdr_kind);
     PIPCK_LAUNCHED("k_gen_ragged");
+    return PIPCK_OK;
+}
+
+int pipck_gen_packed_bytes(void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
+                           uint64_t first_pkt, uint64_t seed, uint32_t hdr_kind, void* stream) {
+    if (!n) return PIPCK_OK;
+    if (!d_arena || !d_lens || !d_tile_off) {
+        set_error("pipck_gen_packed_bytes: null pointer");
+        return PIPCK_EINVAL;
+    }
+    hipLaunchKernelGGL(k_gen_packedb, dim3((uint32_t)((n + 63) / 64)), dim3(64), 0, as_stream(stream),
+                       (uint8_t*)d_arena, d_lens, d_tile_off, n, first_pkt, seed, hdr_kind);
+    PIPCK_LAUNCHED("k_gen_packedb");
     return PIPCK_OK;
 }
 

@@ -308,28 +308,7 @@ __device__ __forceinline__ void trace_task(uint32_t kflags, const TraceBuf& tb, 
 // wave, and since a packet spans >= 64 chunks a row holds at most one packet
 // boundary.  Lanes keep a running u64 sum for the packet the row is in; at a
 // boundary the finished packet's partials are folded and wave-reduced once.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
-// Inclusive wave-64 prefix sum on the DPP crossbar (GFX9 DPP: row_shr inside
-// 16-lane rows, then row_bcast:15 / row_bcast:31 across rows) -- no LDS trips.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
-
-// Wave total as a scalar: the DPP scan's last lane (six VALU steps and one
-// v_readlane; a __shfl_xor butterfly would be six ds_bpermute round trips).
-__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(v), 63);
-}
 
 // A finished packet is not reduced across the wave on the spot: every lane
 // parks its folded partial (16 bits keep the residue and zero-ness) in the
@@ -887,12 +866,6 @@ constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
 constexpr uint32_t kTinyChunks = 2;
 constexpr uint32_t kNoTinyTiles = 1u << 16;  // pipck_tune flags bit 16: tiny tiles take the chunk stream too
 
-// Lane 0's value of a 64-bit quantity, as a scalar (both halves zero-extended).
-__device__ __forceinline__ uint64_t first_lane_u64(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
 
 // Segment of chunk c: the last segment starting at or before c (which skips
 // empty segments).  A lane's chunk advances by 64 per row, so it usually stays
@@ -1001,16 +974,6 @@ __device__ __forceinline__ void ragged_reduce_row(RaggedTileLds& t, uint32_t row
     if (tail || head) atomicAdd(&t.acc[s], (tail ? inc : 0u) - (head ? inc - val : 0u));
 }
 
-// Inclusive wave-64 max-scan (same DPP pattern as wave_incl_scan).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return v;
-}
 
 // Segment ends a mixed row walks in scalar code; beyond this many the row
 // finds its lanes' segments through LDS start marks instead.
@@ -1373,16 +1336,8 @@ struct Tune {
 };
 static Tune g_tune;
 
-// The batch kernel this thread launched last (its host-side handle), so a
-// measurement can name the exact template instantiation it timed
-// (pipck_last_launch in pipck_testing.h: bench.py binds a PMC traffic file to
-// that name).  One thread-local store per launch.
-static thread_local const void* t_last_kernel = nullptr;
-#define PIPCK_LAUNCH(K, ...)                                          \
-    do {                                                              \
-        t_last_kernel = reinterpret_cast<const void*>(K);             \
-        hipLaunchKernelGGL(K, __VA_ARGS__);                           \
-    } while (0)
+// The batch kernel this thread launched last (pipck_common.hpp, PIPCK_LAUNCH).
+thread_local const void* t_last_kernel = nullptr;
 
 typedef void (*fixed_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
                          uint64_t, uint16_t*, uint8_t*);

@@ -1,0 +1,320 @@
+// pipck_packedb.hip -- byte-packed ragged batches (cfg4's bench layout) + their C ABI.
+//
+// Hot path: plumk97/pip pip/pip_checksum.cpp:42-87 (pip_inet{,6}_checksum)
+// over a batch of variable-length segments laid back to back with NO padding:
+// packet i starts at byte b_i = len_0 + ... + len_{i-1} of the arena.  The
+// 16-byte-granular packed layout (pipck_checksum_packed, k_packed) rounds each
+// segment up to 16 bytes; on cfg4's Zipf lengths that padding is 0.76 % of the
+// bytes read, every one of them fetched from HBM.  Here nothing but packet
+// bytes (and the 2-byte lengths) is read.
+//
+// k_packedb: one tile of 64 packets per wave, as in k_packed.  The wave reads
+// its 64 u16 lengths and the tile's byte offset (one u64 per tile), derives
+// every packet's offset with a wave prefix scan, and streams the tile as
+// coalesced 1 KiB rows from the 128-B line holding its first byte (rows are
+// whole lines; the bytes before the tile's first packet belong to the
+// previous tile and are summed into a discarded slot).  Since segments are no
+// longer chunk-aligned, a 16-byte chunk may hold the end of one segment and
+// the start of the next: each lane splits its chunk at that boundary into a
+// low part (the segment holding the chunk's first byte, found by LDS start
+// marks + a DPP max-scan) and a high part (the next segment), and the row
+// reduces by segment with the head/tail prefix-scan trick over the low parts
+// plus one LDS add per boundary lane for the high part.  A row wholly inside
+// one segment is four dot2 ops into a per-lane run partial, nothing else.
+// Segments are summed as little-endian dwords of aligned chunks and byte
+// order is fixed once per segment from its start's parity (pipck_device.hpp).
+//
+// Tiles holding a segment shorter than 16 bytes (where one chunk could hold
+// three segments) are summed lane-per-segment instead: correct for any
+// lengths (0 included), slow, and absent from the BASELINE shapes (>= 64 B).
+#include "pipck_common.hpp"
+#include "pipck_device.hpp"
+
+namespace pipck {
+
+struct PackedbLds {
+    // +1-encoded segment slots: 0 = the bytes before the tile's first packet,
+    // s + 1 = packet s of the tile, nv + 1 .. 65 = bytes after its last packet
+    uint32_t end[66];  // end[S] = byte (relative to the line-aligned base) where slot S ends
+    uint32_t acc[66];  // LE residue partial per slot
+    uint32_t mark[64];  // (row tag << 7) | S of the slot starting at chunk row + i (max wins)
+};
+
+// Add a run of whole rows of one slot (per-lane u32 partials in racc) to the
+// slot's LDS partial: one wave sum, one LDS add.
+__device__ __forceinline__ void packedb_flush(PackedbLds& t, int lane, uint32_t& racc, uint32_t& rslot) {
+    if (rslot == 0xFFFFFFFFu) return;  // wave-uniform
+    const uint32_t tot = wave_total(racc);
+    if (lane == 0) atomicAdd(&t.acc[rslot], tot);
+    racc = 0;
+    rslot = 0xFFFFFFFFu;
+}
+
+// One 1 KiB row (chunks row .. row+63 of the tile stream).  start_v / end_v:
+// lane s holds packet s's first and one-past-last byte (relative); mfirst_v
+// the first chunk whose first byte lies in packet s (start rounded up to 16);
+// nv valid packets.  S0 / e0: the slot holding the row's first byte and its
+// end byte (scalars, carried across rows).
+__device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, uint32_t row, uint32_t total, int lane,
+                                                   const u32x4& v, uint32_t start_v, uint32_t end_v,
+                                                   uint32_t mfirst_v, bool valid, uint32_t nv, uint32_t& S0,
+                                                   uint32_t& e0, uint32_t& racc, uint32_t& rslot) {
+    const uint32_t rb = 16u * row;  // the row's first byte
+    if (rb >= e0) {                 // wave-uniform: the row starts past slot S0
+        S0 = (uint32_t)__popcll(__ballot(valid && start_v <= rb));
+        e0 = t.end[S0];
+    }
+    S0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)S0);
+    e0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)e0);
+    rslot = (uint32_t)__builtin_amdgcn_readfirstlane((int)rslot);
+    if (e0 >= rb + 1024u) {  // interior row: every byte of the row in slot S0
+        if (S0 != rslot) {
+            packedb_flush(t, lane, racc, rslot);
+            rslot = S0;
+        }
+        racc = dot4(v, racc);
+        return;
+    }
+    // the run of whole rows ends here: its wave total joins S0's tail lane
+    // when it is S0's, else it is added on its own
+    uint32_t R = 0;
+    if (rslot != 0xFFFFFFFFu) {
+        R = wave_total(racc);
+        if (rslot != S0) {
+            if (lane == 0) atomicAdd(&t.acc[rslot], R);
+            R = 0;
+        }
+        racc = 0;
+        rslot = 0xFFFFFFFFu;
+    }
+    const uint32_t c = row + lane;
+    const bool active = c < total;
+    // slot of the chunk's first byte: marks of the packets whose first
+    // byte-owned chunk falls in this row, max-scanned from S0 at lane 0
+    const uint32_t tag = ((row >> 6) + 1u) << 7;
+    if (valid && mfirst_v > row && mfirst_v < row + 64) atomicMax(&t.mark[mfirst_v - row], tag | (uint32_t)(lane + 1));
+    wave_sync();
+    const uint32_t m = t.mark[lane];
+    const bool head = lane > 0 && m >= tag;
+    const uint32_t S = wave_incl_max(lane == 0 ? S0 : (m >= tag ? (m & 127u) : 0u));
+    // bytes of this chunk in slot S: [0, p); the rest [p, 16) opens slot S + 1
+    const int p = (int)t.end[S] - 16 * (int)c;  // >= 1
+    const uint32_t val = active ? dot4(v, 0u) : 0u;
+    const uint32_t lo = (p >= 16 || !active) ? val : dot4(mask_tail(v, p), 0u);
+    const uint32_t inc = wave_incl_scan(lo);
+    const bool tail = active && (lane == 63 || p <= 16);
+    const bool hd = active && head;
+    const uint32_t add = (tail ? inc + (S == S0 ? R : 0u) : 0u) - (hd ? inc - lo : 0u);
+    if (tail || hd) atomicAdd(&t.acc[S], add);
+    if (active && p < 16) atomicAdd(&t.acc[S + 1], val - lo);
+    (void)end_v;
+    (void)nv;
+}
+
+template <int U, bool NT>
+__device__ __forceinline__ void packedb_stream(PackedbLds& t, uint32_t total, int lane, uintptr_t base,
+                                               uint32_t start_v, uint32_t end_v, uint32_t mfirst_v, bool valid,
+                                               uint32_t nv) {
+    if (!total) return;
+    // the tile's chunks as a range-checked buffer: reads end at the 16-byte
+    // boundary after the tile's last byte
+    const buf_t tb = buf_rsrc(reinterpret_cast<const void*>(base), total * 16u);
+    u32x4 v[U];
+    uint32_t S0 = 0, e0 = 0, racc = 0, rslot = 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        v[u] = buf_load<NT>(tb, (u * 64u + lane) * 16u);
+        __builtin_amdgcn_sched_barrier(0);  // keep row order
+    }
+    for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t row = c0 + u * 64;
+            if (row < total)  // wave-uniform
+                packedb_reduce_row(t, row, total, lane, v[u], start_v, end_v, mfirst_v, valid, nv, S0, e0, racc,
+                                   rslot);
+            // unconditional reload (past the tile: zeros, no request), so each
+            // reduce waits for its own row only (vmcnt(U-1))
+            v[u] = buf_load<NT>(tb, (row + 64u * U + lane) * 16u);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    packedb_flush(t, lane, racc, rslot);
+}
+
+// Lane-per-segment sum for tiles holding a segment shorter than 16 bytes.
+__device__ __forceinline__ uint32_t packedb_lane_sum(uintptr_t base, uint32_t start, uint32_t len) {
+    if (!len) return 0u;
+    const u32x4* b = reinterpret_cast<const u32x4*>(base);
+    const uint32_t c0 = start >> 4, c1 = (start + len - 1) >> 4;
+    uint32_t acc = 0;
+    for (uint32_t c = c0; c <= c1; c++) {
+        const int lo = c == c0 ? (int)(start & 15u) : 0;
+        const int hi = (int)(start + len) - 16 * (int)c;
+        u32x4 x = load_plain(b + c);
+        if (lo != 0 || hi < 16) x = mask_chunk(x, lo, hi);
+        acc = dot4(x, acc);
+    }
+    return acc;
+}
+
+template <bool VERIFY, int U, bool NT>
+__global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
+                                                const uint64_t* __restrict__ tile_off, uint64_t n,
+                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    __shared__ PackedbLds t;
+    const int lane = threadIdx.x & 63;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t seg = tile * 64 + lane;
+    const bool valid = seg < n;
+    const uint32_t len = valid ? lens[seg] : 0u;
+    uint32_t Pbase = 0;
+    if (pseudo && valid) {  // loaded now so the tile's end waits on nothing
+        const uint32_t f0 = (uint32_t)((flow_origin + tile * 64) % n_flows);
+        Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
+    }
+    const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
+    const uint64_t first = (uint64_t)(uintptr_t)arena + tile_off[tile];
+    const uintptr_t base = (uintptr_t)(first & ~127ull);  // the line holding the tile's first byte
+    const uint32_t excl = wave_incl_scan(len) - len;
+    const uint32_t start = (uint32_t)(first - base) + excl;  // relative to base
+    const uint32_t end = start + len;
+    const uint32_t end_last = (uint32_t)__builtin_amdgcn_readlane((int)end, (int)(nv - 1));
+    // slot ends: slot 0 (lead) ends where packet 0 starts; slot s + 1 at packet s's end
+    if (lane == 0) t.end[0] = (uint32_t)(first - base);
+    t.end[lane + 1] = valid ? end : 0xFFFFFFFFu;  // past the last packet: never ends (trailing bytes)
+    if (lane == 0) t.end[65] = 0xFFFFFFFFu;        // (end[64] is lane 63's: a full tile's last packet)
+    t.acc[lane] = 0;
+    if (lane < 2) t.acc[64 + lane] = 0;
+    t.mark[lane] = 0;
+    wave_sync();
+    uint32_t le;
+    if (__any(valid && len < 16)) {
+        le = valid ? packedb_lane_sum(base, start, len) : 0u;
+    } else {
+        const uint32_t mfirst = (start + 15u) >> 4;  // first chunk whose first byte is in this packet
+        const uint32_t total = (end_last + 15u) >> 4;
+        packedb_stream<U, NT>(t, total, lane, base, start, end, mfirst, valid, nv);
+        wave_sync();
+        le = t.acc[lane + 1];
+    }
+    const uint32_t w = fold16(le);
+    const uint32_t F = (start & 1u) ? w : bswap16(w);  // byte order from the packet's start parity
+    const uint32_t P = pseudo ? Pbase + len : 0u;
+    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    if (VERIFY)  // write-through result stores (store_result16); lanes past the batch are range-checked off
+        store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, r);
+    else
+        store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, r);
+}
+
+// tile_off[t] = bytes of every packet before packet 64 t (the last entry = the
+// batch's bytes): pass 1 sums each tile's lengths into tile_off[t + 1], pass 2
+// (one block) turns them into a prefix in place.
+__global__ __launch_bounds__(64) void k_packedb_tile_sums(const uint16_t* __restrict__ lens, uint64_t n,
+                                                          uint64_t* __restrict__ tile_off) {
+    const uint64_t seg = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    const uint32_t tot = wave_total(seg < n ? lens[seg] : 0u);
+    if (threadIdx.x == 0) tile_off[blockIdx.x + 1] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_packedb_tile_scan(uint64_t* __restrict__ tile_off, uint64_t n_tiles) {
+    __shared__ uint64_t part[1024];
+    const uint32_t i = threadIdx.x;
+    const uint64_t per = (n_tiles + 1023) / 1024, b = min<uint64_t>(n_tiles, i * per), e = min<uint64_t>(n_tiles, b + per);
+    uint64_t s = 0;
+    for (uint64_t k = b; k < e; k++) s += tile_off[k + 1];
+    part[i] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the 1024 partials
+        const uint64_t x = i >= off ? part[i - off] : 0ull;
+        __syncthreads();
+        part[i] += x;
+        __syncthreads();
+    }
+    uint64_t run = part[i] - s;
+    for (uint64_t k = b; k < e; k++) {
+        run += tile_off[k + 1];
+        tile_off[k + 1] = run;
+    }
+    if (i == 0) tile_off[0] = 0;
+}
+
+static int launch_packedb(bool verify, const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off,
+                          uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                          uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, hipStream_t s) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_lens || !d_tile_off || (verify ? !d_ok : !d_out)) {
+        set_error("pipck_checksum_packed_bytes: null pointer");
+        return PIPCK_EINVAL;
+    }
+    if ((uintptr_t)d_arena % 128) {
+        set_error("pipck_checksum_packed_bytes: the arena must be 128-byte aligned");
+        return PIPCK_EINVAL;
+    }
+    if (d_pseudo && !d_flow_of && n_flows == 0) {
+        set_error("pipck_checksum_packed_bytes: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7FFFFFFFull) {
+        set_error("pipck_checksum_packed_bytes: more than 2^37 packets in one launch");
+        return PIPCK_ERANGE;
+    }
+    const uint32_t nf = n_flows ? n_flows : 1u;
+    // a ring of 32 rows, non-temporal loads, as k_packed
+    if (verify)
+        PIPCK_LAUNCH((k_packedb<true, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
+                          (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
+                          d_ok);
+    else
+        PIPCK_LAUNCH((k_packedb<false, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
+                          (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
+                          d_ok);
+    PIPCK_LAUNCHED("k_packedb");
+    return PIPCK_OK;
+}
+
+}  // namespace pipck
+
+using namespace pipck;
+
+extern "C" {
+
+int pipck_checksum_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
+                                const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                                uint64_t flow_origin, uint16_t* d_out, void* stream) {
+    return launch_packedb(false, d_arena, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out,
+                          nullptr, as_stream(stream));
+}
+
+int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
+                              const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                              uint64_t flow_origin, uint8_t* d_ok, void* stream) {
+    return launch_packedb(true, d_arena, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr,
+                          d_ok, as_stream(stream));
+}
+
+int pipck_packed_bytes_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_off, void* stream) {
+    if (!d_tile_off || (n && !d_lens)) {
+        set_error("pipck_packed_bytes_index: null pointer");
+        return PIPCK_EINVAL;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7FFFFFFFull) {
+        set_error("pipck_packed_bytes_index: more than 2^37 packets");
+        return PIPCK_ERANGE;
+    }
+    hipStream_t s = as_stream(stream);
+    if (tiles) {
+        hipLaunchKernelGGL(k_packedb_tile_sums, dim3((uint32_t)tiles), dim3(64), 0, s, d_lens, n, d_tile_off);
+        PIPCK_LAUNCHED("k_packedb_tile_sums");
+    }
+    hipLaunchKernelGGL(k_packedb_tile_scan, dim3(1), dim3(1024), 0, s, d_tile_off, tiles);
+    PIPCK_LAUNCHED("k_packedb_tile_scan");
+    return PIPCK_OK;
+}
+
+}  // extern "C"

@@ -166,7 +166,7 @@ def packed_index(lens, n: int | None = None):
 _packed_total: dict = {}  # id(tile_chunk) -> (weakref, tensor version, n, chunks)
 
 
-def _check_packed(arena, lens, tile_chunk, n):
+def _check_packed(arena, lens, tile_chunk, n, unit: int = 16):
     """Host-side guard: the batch must lie inside the arena.  The index's total
     (tile_chunk[ceil(n/64)], one device read) is cached on the index tensor
     OBJECT and its in-place version counter, never on addresses: a freed tensor's
@@ -185,8 +185,44 @@ def _check_packed(arena, lens, tile_chunk, n):
         if len(_packed_total) > 64:
             _packed_total.clear()
         _packed_total[id(tile_chunk)] = (weakref.ref(tile_chunk), tile_chunk._version, n, chunks)
-    if 16 * chunks > arena.numel() * arena.element_size():
-        raise ValueError(f"packed batch needs {16 * chunks} B, arena has {arena.numel() * arena.element_size()}")
+    need = unit * chunks if unit == 16 else (chunks + 15) // 16 * 16  # bytes: read to the next 16-B boundary
+    if need > arena.numel() * arena.element_size():
+        raise ValueError(f"packed batch needs {need} B, arena has {arena.numel() * arena.element_size()}")
+
+
+def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
+                          flow_origin: int = 0, out=None):
+    """Byte-packed ragged batch (pipck_checksum_packed_bytes): packets back to back with no padding,
+    lens = device int16/uint16 lengths, tile_off = packed_bytes_index(lens); arena 128-byte aligned."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    _check_packed(arena, lens, tile_off, n, unit=1)
+    call("pipck_checksum_packed_bytes", _ptr(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo), n_flows,
+         _ptr(flow_of), flow_origin, _ptr(out), current_stream(arena.device))
+    return out
+
+
+def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
+                        flow_origin: int = 0, ok=None):
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check_packed(arena, lens, tile_off, n, unit=1)
+    call("pipck_verify_packed_bytes", _ptr(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo), n_flows,
+         _ptr(flow_of), flow_origin, _ptr(ok), current_stream(arena.device))
+    return ok
+
+
+def packed_bytes_index(lens, n: int | None = None):
+    """tile_off for a byte-packed batch: the byte offset of every 64th packet (u64 as int64) + the total."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    to = torch.empty((n + 63) // 64 + 1, dtype=torch.int64, device=lens.device)
+    call("pipck_packed_bytes_index", _ptr(lens), n, _ptr(to), current_stream(lens.device))
+    return to
 
 
 def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
@@ -269,6 +305,24 @@ def gen_packed(n: int, first: int, seed: int, hdr: int, device=None, lengths=Non
     del desc
     lens16 = lengths.to(torch.int16)
     return arena, lens16, packed_index(lens16, n), lengths
+
+
+def gen_packed_bytes(n: int, first: int, seed: int, hdr: int, device=None, lengths=None):
+    """Zipf-length batch (cfg4 shape) in the byte-packed layout: (arena, lens u16-in-int16, tile_off, lengths i32).
+    Packet bytes equal gen_ragged's packet for packet; only the 16-byte padding between packets is gone."""
+    torch = _torch()
+    dev = device or "cuda"
+    if lengths is None:
+        lengths = torch.empty(n, dtype=torch.int32, device=dev)
+        call("pipck_gen_zipf_lengths", _ptr(lengths), n, first, seed, current_stream(lengths.device))
+    lens16 = lengths.to(torch.int16)
+    tile_off = packed_bytes_index(lens16, n)
+    total = int(tile_off[(n + 63) // 64].item())
+    arena = torch.empty(max((total + 15) // 16 * 16, 16), dtype=torch.uint8, device=lengths.device)
+    arena[total:].zero_()  # the bytes after the last packet, up to the 16-B boundary the kernel reads to
+    call("pipck_gen_packed_bytes", _ptr(arena), _ptr(lens16), _ptr(tile_off), n, first, seed, hdr,
+         current_stream(arena.device))
+    return arena, lens16, tile_off, lengths
 
 
 def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, plain_loads: bool = False,

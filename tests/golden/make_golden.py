@@ -176,6 +176,8 @@ EDGES = {
     "edge_flat32_udp6": {"cfg": 3, "n": 48, "ck_every": 2, "ck_off": 6, "kernel": "k_flat<32,"},
     "edge_small_ip20": {"cfg": 1, "n": 4096, "ck_every": 5, "ck_off": 10, "zero_every": 7, "kernel": "k_small<"},
     "edge_packed_tcp4": {"cfg": 4, "n": 4096, "ck_every": 2, "ck_off": 16, "zero_every": 0, "kernel": "k_packed<"},
+    "edge_packedb_tcp4": {"cfg": 4, "n": 4096, "ck_every": 3, "ck_off": 16, "zero_every": 0, "layout": "bytes",
+                          "kernel": "k_packedb<"},
     "edge_flat_len0_v4": {"cfg": 2, "n": 256, "stride": 1024, "length": 0, "proto": 0, "zero_flows_every": 4,
                           "kernel": "k_flat<24,"},
 }
@@ -190,7 +192,9 @@ def edge_inputs_cpu(orc, b: dict):
     rec = 12 if fam == 4 else 36
     for k in b["zero_flows"]:
         flows[rec * k:rec * k + rec - 4] = bytes(rec - 4)
-    if w.ragged:
+    if w.ragged and b.get("layout") == "bytes":
+        arena, offs, lens = orc.gen_packed_bytes_batch(b["seed"], b["first"], n, b["hdr"])
+    elif w.ragged:
         arena, offs, lens = orc.gen_ragged_batch(b["seed"], b["first"], n, b["hdr"])
     else:
         st, L = b["stride"], b["length"]
@@ -231,7 +235,10 @@ def edge_batch(orc, ref, name: str, spec: dict) -> dict:
     for k in zero_flows:
         flows[rec * k:rec * k + rec - 4] = bytes(rec - 4)  # src, dst (proto stays)
     flows = bytes(flows)
-    if w.ragged:
+    if w.ragged and spec.get("layout") == "bytes":
+        arena, offs, lens = orc.gen_packed_bytes_batch(w.seed, first, n, w.hdr)
+        stride, length = 0, None
+    elif w.ragged:
         arena, offs, lens = orc.gen_ragged_batch(w.seed, first, n, w.hdr)
         stride, length = 0, None
     else:
@@ -264,7 +271,8 @@ def edge_batch(orc, ref, name: str, spec: dict) -> dict:
     assert n_zero + n_ffff > 0, name
     return {"cfg": w.cfg, "n": n, "first": first, "seed": w.seed, "stride": stride, "length": length, "hdr": w.hdr,
             "family": fam, "proto": proto, "n_flows": N_FLOWS, "zero_flows": zero_flows, "patches": patches,
-            "kernel": spec["kernel"], "arena_sha256": sha(arena), "results_sha256": sha(out.astype("<u2")),
+            "kernel": spec["kernel"], "layout": spec.get("layout", "padded16" if w.ragged else "fixed"),
+            "arena_sha256": sha(arena), "results_sha256": sha(out.astype("<u2")),
             "head": [int(x) for x in out[:16]], "n_zero": n_zero, "n_ffff": n_ffff}
 
 
@@ -292,8 +300,10 @@ def main() -> None:
             ref_out = np.array([ref.inet_checksum(arena[int(o):int(o) + int(L)].tobytes(), w.proto,
                                                   *orc.flow4(w.seed, (first + i) % N_FLOWS), int(L))
                                 for i, (o, L) in enumerate(zip(offs, lens))], dtype=np.uint16)
+            # the byte-packed layout the bench runs (pipck_checksum_packed_bytes): same packets, no padding
+            ab, _, _ = orc.gen_packed_bytes_batch(w.seed, first, n, w.hdr)
             extra = {"lengths_sha256": sha(lens.astype("<u4")), "mean_len": float(lens.mean()),
-                     "arena_bytes": int(arena.size)}
+                     "arena_bytes": int(arena.size), "arena_bytes_sha256": sha(ab)}
         else:
             arena = orc.gen_fixed_batch(w.seed, first, n, w.length, w.hdr, w.stride)
             want = orc.batch_fixed(arena, w.stride, w.length, n, w.family, w.proto, w.seed, N_FLOWS, first)

@@ -181,7 +181,7 @@ def last_kernel() -> str:
 
 
 # the kernel each config's bench launch runs: the fixture pins THAT kernel
-BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat<32,", 4: "k_packed<", 5: "k_flat<32,"}
+BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat<32,", 4: "k_packedb<", 5: "k_flat<32,"}
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
@@ -194,9 +194,13 @@ def test_batch_kernel_reproduces_pips_results(batches, name):
     assert b["stride"] == w.stride
     pseudo = _pseudo(w)
     if w.ragged:
-        arena, lens16, tc, _ = engine.gen_packed(b["n"], b["first"], b["seed"], b["hdr"])
-        outs = {"packed": engine.checksum_packed(arena, lens16, tc, b["n"], pseudo, N_FLOWS, None, b["first"])}
+        ab, lb, to, _ = engine.gen_packed_bytes(b["n"], b["first"], b["seed"], b["hdr"])
+        assert sha(ab.cpu().numpy()) == b["arena_bytes_sha256"]  # the byte-packed arena pip's results are over
+        outs = {"packed_bytes": engine.checksum_packed_bytes(ab, lb, to, b["n"], pseudo, N_FLOWS, None, b["first"])}
         kernel = last_kernel()
+        arena, lens16, tc, _ = engine.gen_packed(b["n"], b["first"], b["seed"], b["hdr"])
+        outs["packed16"] = engine.checksum_packed(arena, lens16, tc, b["n"], pseudo, N_FLOWS, None, b["first"])
+        assert "k_packed<" in last_kernel()
         _, desc, _ = _device_batch(b, w)
         outs["ragged"] = engine.checksum_ragged(arena, desc, pseudo)
         assert "k_ragged<" in last_kernel()
@@ -224,7 +228,9 @@ def test_edge_fixture_through_batch_kernel(batches, name):
     b = batches[name]
     w = next(x for x in ALL.values() if x.cfg == b["cfg"])
     n, fam = b["n"], b["family"]
-    if w.ragged:
+    if w.ragged and b.get("layout") == "bytes":
+        arena, lens16, tc, _ = engine.gen_packed_bytes(n, b["first"], b["seed"], b["hdr"])
+    elif w.ragged:
         arena, lens16, tc, _ = engine.gen_packed(n, b["first"], b["seed"], b["hdr"])
     elif b["length"]:
         arena = torch.empty(n * b["stride"], dtype=torch.uint8, device=DEV)
@@ -242,7 +248,9 @@ def test_edge_fixture_through_batch_kernel(batches, name):
         if b["zero_flows"]:
             flows.view(b["n_flows"], rec)[torch.tensor(b["zero_flows"], device=DEV), :rec - 4] = 0
         pseudo = engine.prepare_flows(fam, flows, b["n_flows"])
-    if w.ragged:
+    if w.ragged and b.get("layout") == "bytes":
+        out = engine.checksum_packed_bytes(arena, lens16, tc, n, pseudo, b["n_flows"], None, b["first"])
+    elif w.ragged:
         out = engine.checksum_packed(arena, lens16, tc, n, pseudo, b["n_flows"], None, b["first"])
     else:
         out = engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None, b["first"])
@@ -975,6 +983,129 @@ def test_full_size_packed(oracle):
     again = engine.checksum_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 0)
     assert int((again != 0).sum().item()) == 0
     assert bool((engine.verify_packed(arena, lens16, tc, n, pseudo, N_FLOWS, None, 0) == 1).all())
+    del arena, out, again
+    torch.cuda.empty_cache()
+
+
+# ----------------------------------------------------------------------------
+# 8b. byte-packed ragged batches (pipck_checksum_packed_bytes: cfg4's bench layout)
+# ----------------------------------------------------------------------------
+def _packedb_upload(rng, lens, lead=0):
+    """Host + device arena in the byte-packed layout (packets back to back, no
+    padding; `lead` random bytes before packet 0 via a shifted index is not
+    possible -- the index starts at 0 -- so the arena itself is 128-B aligned
+    and the first tile starts on a line); bytes after the last packet up to the
+    16-B boundary are random too.  Returns (host, offsets, arena, lens16, tile_off)."""
+    offs = np.zeros(len(lens), dtype=np.uint64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(lens.astype(np.uint64))[:-1]
+    total = int(lens.astype(np.uint64).sum())
+    host = rng.integers(0, 256, (total + 15) // 16 * 16 + 16, dtype=np.uint8)
+    _, arena = upload(host, 0)
+    lens16 = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(DEV)
+    to = engine.packed_bytes_index(lens16)
+    want = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))])[::64]
+    got = to.cpu().numpy()
+    assert np.array_equal(got[:-1], want[:len(got) - 1]) and got[-1] == total
+    return host, offs, arena, lens16, to
+
+
+@pytest.mark.parametrize("shape", ["zipf", "uniform", "tiny", "short", "mixed", "jumbo", "edge", "sixteen"])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 3001])
+def test_packed_bytes_vs_oracle(oracle, shape, n):
+    """Byte-packed batches: segments at every byte alignment (odd starts swap
+    pip's byte pairing), chunks split between two segments, rows wholly inside
+    one segment, tiles with a segment under 16 bytes (lane-per-segment path),
+    empty segments; implicit / explicit flows and no pseudo-header; RX verify."""
+    rng = np.random.default_rng(hash(("b", shape, n)) % 2**32)
+    if shape == "sixteen":  # the smallest lengths the chunk stream takes
+        lens = rng.choice([16, 17, 18, 31, 32, 33, 47], n).astype(np.uint32)
+    else:
+        lens = _packed_lens(rng, shape, n, oracle)
+    host, offs, arena, lens16, to = _packedb_upload(rng, lens)
+    for fam, explicit in ((4, False), (6, True), (0, False)):
+        seed, proto, origin = 77 + n, 6 if fam == 4 else 17, int(rng.integers(0, 1 << 40))
+        pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+        flow_of = None
+        flow_idx = (origin + np.arange(n)) % N_FLOWS
+        if explicit:
+            flow_idx = rng.integers(0, N_FLOWS, n)
+            flow_of = torch.from_numpy(flow_idx.astype(np.int32)).to(DEV)
+        if fam == 0:
+            want = np.array([oracle.ip_checksum(host[int(o):int(o) + int(L)].tobytes()) for o, L in zip(offs, lens)],
+                            dtype=np.uint16)
+        elif explicit:
+            want = np.array([oracle.inet6_checksum(host[int(o):int(o) + int(L)].tobytes(), proto,
+                                                   *oracle.flow6(seed, int(f)), int(L))
+                             for o, L, f in zip(offs, lens, flow_idx)], dtype=np.uint16)
+        else:
+            want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
+        got = u16(engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, flow_of,
+                                               0 if explicit else origin))
+        assert "k_packedb<" in last_kernel()
+        ok = engine.verify_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, flow_of,
+                                        0 if explicit else origin).cpu().numpy().astype(bool)
+        assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
+        assert np.array_equal(ok, got == 0)
+
+
+def test_packed_bytes_equals_packed_on_the_same_packets(oracle):
+    """The byte-packed and the 16-B-granular layouts of one Zipf batch give the
+    same results (device generators: same packet bytes, different padding)."""
+    w, n = CFG4, 200_003
+    a16, l16, tc, lens = engine.gen_packed(n, 5, w.seed, w.hdr)
+    ab, lb, to, lens_b = engine.gen_packed_bytes(n, 5, w.seed, w.hdr)
+    assert torch.equal(lens, lens_b)
+    assert ab.numel() == (int(lens.to(torch.int64).sum().item()) + 15) // 16 * 16
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    x = engine.checksum_packed(a16, l16, tc, n, pseudo, N_FLOWS, None, 5)
+    y = engine.checksum_packed_bytes(ab, lb, to, n, pseudo, N_FLOWS, None, 5)
+    assert torch.equal(x, y)
+    host, offs, hl = oracle.gen_packed_bytes_batch(w.seed, 5, 3000, w.hdr)
+    assert np.array_equal(ab[:len(host)].cpu().numpy()[:int(offs[-1] + hl[-1])], host[:int(offs[-1] + hl[-1])])
+
+
+def test_packed_bytes_argument_checks():
+    lens16 = torch.full((10,), 20, dtype=torch.int16, device=DEV)
+    to = engine.packed_bytes_index(lens16)
+    arena = torch.zeros(512, dtype=torch.uint8, device=DEV)
+    lib = _lib.load()
+    out = torch.empty(10, dtype=torch.int16, device=DEV)
+    rc = lib.pipck_checksum_packed_bytes(C.c_void_p(arena.data_ptr() + 16), C.c_void_p(lens16.data_ptr()),
+                                         C.c_void_p(to.data_ptr()), 10, None, 1, None, 0,
+                                         C.c_void_p(out.data_ptr()), None)
+    assert rc == _lib.PIPCK_EINVAL  # not 128-byte aligned
+    with pytest.raises(ValueError):  # the index says more bytes than the arena holds
+        big = torch.full((10,), 100, dtype=torch.int16, device=DEV)
+        engine.checksum_packed_bytes(arena[:960 - 512], big, engine.packed_bytes_index(big))
+
+
+def test_full_size_packed_bytes(oracle):
+    """cfg4 at its BASELINE size in the byte-packed layout (the bench's path):
+    equal to the descriptor kernel on the same packets, sampled against the
+    oracle, and checksum-of-checksum over the whole batch."""
+    w, n = CFG4, 8 << 20
+    arena, lens16, to, lens = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    out = engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+    got = u16(out)
+    L = lens.cpu().numpy().astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(L.astype(np.uint64))[:-1]
+    desc = engine.make_desc(offs, L, np.arange(n) % N_FLOWS)
+    assert np.array_equal(got, u16(engine.checksum_ragged(arena, desc, pseudo)))
+    del desc
+    rng = np.random.default_rng(45)
+    for i in rng.choice(n, 1500, replace=False):
+        pkt = oracle.packet(w.seed, int(i), int(L[i]), w.hdr)
+        assert got[i] == oracle.inet_checksum(pkt, w.proto, *oracle.flow4(w.seed, int(i) % N_FLOWS)), int(i)
+    o = torch.from_numpy(offs.astype(np.int64)).to(DEV) + 16
+    v = out.to(torch.int32) & 0xFFFF
+    arena[o] = (v >> 8).to(torch.uint8)
+    arena[o + 1] = (v & 0xFF).to(torch.uint8)
+    again = engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+    assert int((again != 0).sum().item()) == 0
+    assert bool((engine.verify_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0) == 1).all())
     del arena, out, again
     torch.cuda.empty_cache()
 

@@ -45,7 +45,8 @@ def main():
     ap.add_argument("--only", default="", help="comma list of cfgN (default cfg5,cfg4)")
     ap.add_argument("--sizes", default="", help="comma list of packet counts in Mi (default per workload)")
     ap.add_argument("--pseudo", action="store_true", help="fixed-stride workloads: add IPv4 pseudo-headers even for cfg1")
-    ap.add_argument("--packed", action="store_true", help="ragged workloads: the packed-lengths kernel (bench.py's)")
+    ap.add_argument("--packed", action="store_true", help="ragged workloads: the 16-B packed-lengths kernel")
+    ap.add_argument("--packedb", action="store_true", help="ragged workloads: the byte-packed kernel (bench.py's)")
     ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs}, or @file (default: built-in arms)")
     a = ap.parse_args()
     engine.require_gpu()
@@ -59,7 +60,11 @@ def main():
         fam = w.family or (4 if a.pseudo else 0)  # cfg1: IP header, no pseudo-header
         pseudo = engine.gen_flows(fam, N_FLOWS, w.seed, w.proto or 6)[1] if fam else None
         for n in sizes:
-            if w.ragged and a.packed:  # the packed layout bench.py runs (u16 lengths + per-64 index)
+            if w.ragged and a.packedb:  # the byte-packed layout bench.py runs (u16 lengths + per-64 byte offset)
+                arena, lens16, tile_off, lens = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+                nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
+                run = lambda: engine.checksum_packed_bytes(arena, lens16, tile_off, n, pseudo, N_FLOWS)  # noqa: E731
+            elif w.ragged and a.packed:  # the 16-B packed layout (u16 lengths + per-64 index)
                 arena, lens16, tile_chunk, lens = engine.gen_packed(n, 0, w.seed, w.hdr)
                 nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
                 run = lambda: engine.checksum_packed(arena, lens16, tile_chunk, n, pseudo, N_FLOWS)  # noqa: E731
