@@ -328,11 +328,13 @@ constexpr uint32_t kLoadsOnly = 1u << 21;
 // tune flags bit 22 (MEASUREMENT ONLY, no results): k_flat skips its task end
 // (the per-packet LDS sums, pseudo-header add and result stores)
 constexpr uint32_t kNoTaskEnd = 1u << 22;
-// bit 23: k_flat's task end computes every result but stores none;
-// bit 28: every task stores its results into the batch's FIRST 64 slots (one
-// 128-B line shared by all waves; both MEASUREMENT ONLY, wrong results)
+// bit 23: k_flat's task end computes every result but stores none
+// (MEASUREMENT ONLY, no results)
 constexpr uint32_t kEndNoStore = 1u << 23;
-constexpr uint32_t kEndSameLine = 1u << 28;
+// bit 28 (same results): the other fixed-stride schedule -- k_flat for jumbo
+// strides (default: the block-cooperative k_flat_coop, pipck_coop.hip),
+// k_flat_coop for shorter ones (default: k_flat)
+constexpr uint32_t kFlatAltSchedule = 1u << 28;
 // EXPERIMENTAL (same results): bit 30 = per-wave result stores (the r02 scheme) instead of one coalesced
 // store of the whole block's results by its last wave; bit 31 = wave tasks of
 // exactly the packet count the heuristic names, not rounded to a multiple of 16
@@ -380,7 +382,7 @@ __device__ __forceinline__ void flat_write(const uint16_t* part, uint32_t pitch,
     for (int j = 0; j < 64; j++) s += part[j * pitch + lane];
     const uint32_t F = bswap16(fold16(s));  // packets start 16-byte aligned: even address
     const uint32_t P = has_pseudo ? Pb + lterm : 0u;
-    const uint64_t pkt = (kflags & kEndSameLine) ? (uint64_t)lane : p0 + lane;
+    const uint64_t pkt = p0 + lane;
     const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
     if (!TO_LDS && (kflags & kEndNoStore) && (uint64_t)r != magic) return;  // measurement: never stores
     if (TO_LDS) {
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
     // cfg5 1.5 % -- as much as the whole task end -- while the same stores all
     // aimed at one line cost nothing (profiles/r03_flat_end_probe.jsonl).  With
     // run a multiple of 16 (launch_fixed) a block's results are whole lines.
-    const bool coalesce = !(kflags & (kFlatWaveStores | kXcdGroups | kEndSameLine)) && (uint64_t)gridDim.x * WPB >= n_tasks;
+    const bool coalesce = !(kflags & (kFlatWaveStores | kXcdGroups)) && (uint64_t)gridDim.x * WPB >= n_tasks;
     uint16_t* bres = s_part + WPB * 64u * pitch;                       // WPB * run u16
     uint32_t* bcnt = reinterpret_cast<uint32_t*>(bres + ((WPB * run + 1u) & ~1u));
     if (coalesce) {
@@ -1513,6 +1515,16 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
+        // Jumbo strides (>= 4 KiB, cfg3 / cfg5) take the block-cooperative stream
+        // (a block's four waves on interleaved rows of one task): cfg5 +0.6 %
+        // at 8M packets and +1.7 % at 1M, cfg3 +0.9 % at 1M over k_flat, on
+        // one box, one process (profiles/r03_flat_coop_scan.jsonl); at 1,488-B
+        // strides the two are even within 0.5 %, so cfg2 keeps k_flat.
+        const bool coop = (cpp >= 256) != ((g_tune.flags.load() & kFlatAltSchedule) != 0);
+        if (coop && stride <= 65536 &&
+            launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, d_ok,
+                             as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load()) == PIPCK_OK)
+            return PIPCK_OK;
         // Rows in flight per wave and task size.  Jumbo packets (>= 4 KiB, cfg3
         // and cfg5): a ring of 32 rows (191 VGPRs, 2 waves/SIMD) over ~128-row
         // tasks, +1.9 % on cfg5 (7.12 TB/s) and +3.5 % on cfg3 over a ring of 16

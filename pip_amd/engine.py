@@ -331,7 +331,7 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          small: bool = True, small_k_log: int = 0, flat_small: bool = True, tiny_tiles: bool = True,
          flat_tiny: bool = True, force_flat_tiny: bool = False, packed_marks_only: bool = False,
          trace: bool = False, loads_only: bool = False, no_task_end: bool = False,
-         end_no_store: bool = False, end_same_line: bool = False,
+         end_no_store: bool = False, alt_flat_schedule: bool = False,
          plain_result_stores: bool = False, wave_stores: bool = False, free_run: bool = False,
          packed_no_align: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
@@ -344,7 +344,7 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
              | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0) | (1 << 22 if no_task_end else 0)
-             | (1 << 23 if end_no_store else 0) | (1 << 28 if end_same_line else 0)
+             | (1 << 23 if end_no_store else 0) | (1 << 28 if alt_flat_schedule else 0)
              | (1 << 29 if plain_result_stores else 0) | (1 << 30 if (wave_stores or packed_no_align) else 0)
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)

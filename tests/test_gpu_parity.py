@@ -181,7 +181,7 @@ def last_kernel() -> str:
 
 
 # the kernel each config's bench launch runs: the fixture pins THAT kernel
-BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat<32,", 4: "k_packedb<", 5: "k_flat<32,"}
+BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
@@ -339,7 +339,9 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
     try:
         for stride, length in cases:
             for blocks in (0, 1, 7, 9, 17):  # < 8 blocks: one group; 9/17: uneven XCD groups
-                engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, xcd_groups=xcd)
+                # k_flat itself at every stride (jumbo strides default to k_flat_coop)
+                engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, xcd_groups=xcd,
+                            alt_flat_schedule=stride >= 4096)
                 n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
                 host = rng.integers(0, 256, n * stride, dtype=np.uint8)
                 if n > 2:
@@ -349,11 +351,43 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
                 seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
                 pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
                 got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+                assert "k_flat<" in last_kernel()
                 want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
                 assert np.array_equal(got, want), (stride, length, n, blocks, np.nonzero(got != want)[0][:5])
                 ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
                 # a packet verifies exactly when its recomputed checksum is 0x0000
                 assert np.array_equal(ok.astype(bool), got == 0)
+    finally:
+        engine.tune()
+
+
+@pytest.mark.parametrize("ring", [17, 25, 33])
+@pytest.mark.parametrize("rows", [0, 2, 48, 96])
+def test_flat_coop_kernel_vs_oracle(oracle, ring, rows):
+    """The block-cooperative flat stream (k_flat_coop, tune bit 28): a block's
+    waves on interleaved rows of one task of K packets; boundaries at every
+    lane, padding chunks, tasks cut short, tiny and large tasks."""
+    rng = np.random.default_rng(ring * 100 + rows)
+    cases = [(1024, 1024), (1024, 1023), (1024, 0), (1040, 1025), (1488, 1480), (1504, 1480), (2048, 17),
+             (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
+    try:
+        for stride, length in cases:
+            # the coop stream is the default for jumbo strides, the alternative below 4 KiB
+            engine.tune(0, ring, 0, alt_flat_schedule=stride < 4096, rows_per_task=rows)
+            n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 700))
+            host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+            if n > 2:
+                host[stride:2 * stride] = 0xFF
+            _, arena = upload(host, 0)
+            fam = int(rng.choice([0, 4, 6]))
+            seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
+            pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+            got = u16(engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin))
+            assert "k_flat_coop<" in last_kernel()
+            want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
+            assert np.array_equal(got, want), (stride, length, n, np.nonzero(got != want)[0][:5])
+            ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
+            assert np.array_equal(ok.astype(bool), got == 0)
     finally:
         engine.tune()
 
