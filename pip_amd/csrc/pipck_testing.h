@@ -37,10 +37,23 @@ extern "C" {
  * packed ragged tiles always find segments through LDS marks (default: a scalar
  * loop over up to 4 segment ends per row).  The packed-batch kernel
  * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32.
- * Bit 20 = record the per-task timeline (pipck_trace_tasks below).  Bit 21 =
- * MEASUREMENT ONLY, WRONG RESULTS: the flat-stream kernel waits for and
- * consumes every row with one add and does no per-packet work (times the
- * access pattern alone).  Bits 22, 23 and 28..31 are unused. */
+ * Bit 20 = record the per-task timeline (pipck_trace_tasks below).
+ * Bit 21 = MEASUREMENT ONLY, WRONG RESULTS: k_flat waits for and consumes every
+ * row with one add and does no per-packet work (times the access pattern
+ * alone).  Bit 22 = MEASUREMENT ONLY, NO RESULTS: k_flat skips its task end.
+ * Bit 23 = MEASUREMENT ONLY, NO RESULTS: k_flat computes its results but stores
+ * none (bits 21-23 isolate the task-end cost, profiles/r03_flat_end_probe.jsonl).
+ * Bit 28 = the other fixed-stride schedule: k_flat for jumbo strides (default
+ * there: the block-cooperative k_flat_coop), k_flat_coop for shorter ones
+ * (default there: k_flat); for k_flat_coop, bits 8..15 are rows per wave and
+ * loads_per_lane 17/25/33 its ring.  Bit 29 = result stores with the r02
+ * write-back policy in k_flat / k_packed instead of write-through (sc1).
+ * Bit 30 = the r02 schemes: per-wave result stores in k_flat (default: one
+ * coalesced store per block), tile rows from the tile's first chunk in k_packed
+ * (default: from its 128-B line).  Bit 31 = k_flat tasks of exactly the packet
+ * count the rows knob gives (default: a multiple of 16 for strides < 4 KiB).
+ * Bits 24..27 = the small kernel's depth (above).  Bits 29-31 compute the same
+ * results; they exist for the separate-process A/Bs recorded in profiles/. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the

@@ -336,7 +336,7 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          packed_no_align: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
-    except loads_only (bit 21), a measurement-only probe of the flat kernel's access pattern."""
+    except the measurement-only probes loads_only (bit 21), no_task_end (22) and end_no_store (23)."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)

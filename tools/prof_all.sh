@@ -13,7 +13,7 @@ for spec in ${WLS:-cfg1:268435456 cfg1 cfg2 cfg3 cfg4 cfg5}; do
     WL=$wl bash tools/profile.sh || exit $?
   fi
 done
-for wl in ${SQ_WLS:-cfg2 cfg4}; do
+for wl in ${SQ_WLS:-cfg2 cfg4 cfg5}; do
   WL=$wl bash tools/sq_profile.sh || exit $?
 done
 echo "== prof_all done"
