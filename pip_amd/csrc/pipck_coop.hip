@@ -29,6 +29,11 @@
 
 namespace pipck {
 
+// pipck_tune flags bits 21 / 22 (MEASUREMENT ONLY, no results), as for k_flat:
+// consume every row with one add and skip the per-row work / skip the task end
+constexpr uint32_t kCoopLoadsOnly = 1u << 21;
+constexpr uint32_t kCoopNoEnd = 1u << 22;
+
 template <int U>
 constexpr int coop_waves_per_simd() { return U >= 32 ? 2 : (U >= 24 ? 3 : (U >= 16 ? 4 : 5)); }
 
@@ -38,7 +43,7 @@ template <int U, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void k_flat_coop(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
     extern __shared__ uint32_t s_part[];  // 64 lanes x pitch u32 (launch_coop sizes it)
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -66,13 +71,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_
     uint32_t pkt = (64u * w) / cpp, k0 = (64u * w) % cpp;
     const uint32_t my_rows = rows > w ? (rows - w + 3) >> 2 : 0u;
     u32x4 v[U];
+    uint32_t probe = 0;
 #pragma unroll
     for (int u = 0; u < U; u++) v[u] = buf_load<NT>(tb, ((w + 4u * u) * 64u + lane) * 16u);  // past the task: zeros
     for (uint32_t j0 = 0; j0 < my_rows; j0 += U) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t j = j0 + u;
-            if (j < my_rows) {  // wave-uniform
+            if (j < my_rows && (kflags & kCoopLoadsOnly)) {  // measurement: consume the row, no per-row work
+                probe += v[u].x;
+            } else if (j < my_rows) {  // wave-uniform
                 // lane's chunk: k0 + lane chunks into packet pkt (at most one boundary: cpp >= 64)
                 uint32_t k = k0 + lane, pk = pkt;
                 if (k >= cpp) {
@@ -97,6 +105,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_
         }
     }
     __syncthreads();
+    if (kflags & (kCoopLoadsOnly | kCoopNoEnd)) {  // measurement only: no results
+        if (probe == 0x9E3779B9u) s_part[0] = probe;
+        return;
+    }
     const uint32_t i = threadIdx.x;
     if (i < np) {
         uint32_t s = 0;
@@ -112,7 +124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_
 }
 
 typedef void (*coop_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*);
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
 
 // Launch for an aligned arena, 16-B-multiple stride in [1 KiB, 64 KiB], len <=
 // stride (checked by the caller).  rows_per_wave: task size target (0 = auto);
@@ -120,7 +132,8 @@ typedef void (*coop_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, 
 // when the shape does not fit a block task (the caller then uses k_flat).
 int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
                      const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
-                     uint16_t* d_out, uint8_t* d_ok, hipStream_t s, uint32_t rows_per_wave, uint32_t ring) {
+                     uint16_t* d_out, uint8_t* d_ok, hipStream_t s, uint32_t rows_per_wave, uint32_t ring,
+                     uint32_t kflags) {
     const uint32_t cpp = (uint32_t)(stride / 16);
     const bool jumbo = cpp >= 256;
     // rows per wave: 64 for jumbo packets (cfg5: 24 packets per block task;
@@ -142,7 +155,7 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
         {k_flat_coop<32, false, true>, k_flat_coop<32, true, true>}};
     const int ui = u >= 32 ? 2 : (u >= 24 ? 1 : 0);
     PIPCK_LAUNCH(kCoop[ui][verify], dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, len, n,
-                 K, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok);
+                 K, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, kflags);
     PIPCK_LAUNCHED("k_flat_coop");
     return PIPCK_OK;
 }

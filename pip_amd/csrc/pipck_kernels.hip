@@ -1523,7 +1523,8 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const bool coop = (cpp >= 256) != ((g_tune.flags.load() & kFlatAltSchedule) != 0);
         if (coop && stride <= 65536 &&
             launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, d_ok,
-                             as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load()) == PIPCK_OK)
+                             as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load(),
+                             g_tune.flags.load()) == PIPCK_OK)
             return PIPCK_OK;
         // Rows in flight per wave and task size.  Jumbo packets (>= 4 KiB, cfg3
         // and cfg5): a ring of 32 rows (191 VGPRs, 2 waves/SIMD) over ~128-row
