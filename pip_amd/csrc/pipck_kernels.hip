@@ -1572,6 +1572,15 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         PIPCK_LAUNCHED("k_flat_small");
         return PIPCK_OK;
     }
+    // Packed 20/24-byte items with no pseudo-header (IPv4 headers, cfg1): rows
+    // of whole headers streamed like the large-packet kernels (pipck_hdr.hip).
+    // pipck_tune loads_per_lane 8/16/24/32 = its ring, 1 = never (k_small instead).
+    if (!d_pseudo && (stride == 20 || stride == 24) && !g_tune.lanes.load() && g_tune.loads.load() != 1) {
+        const uint32_t lq = g_tune.loads.load(), flags = g_tune.flags.load();
+        if (launch_hdr(verify, d_arena, stride, len, n, d_out, d_ok, as_stream(stream), (flags >> 8) & 0xFFu,
+                       lq == 8 || lq == 16 || lq == 24 || lq == 32 ? lq : 0u, nt_for(true), flags) == PIPCK_OK)
+            return PIPCK_OK;
+    }
     // Tiny 8-B-multiple strides with pseudo-headers (pure ACKs, small UDP) or
     // RX verify: the LDS-staged row stream.  cfg1 on 24-B strides, 256M
     // packets: with IPv4 pseudo-headers 1.29 vs 1.40 ms for k_small (+8.5 %),

@@ -53,7 +53,12 @@ extern "C" {
  * (default: from its 128-B line).  Bit 31 = k_flat tasks of exactly the packet
  * count the rows knob gives (default: a multiple of 16 for strides < 4 KiB).
  * Bits 24..27 = the small kernel's depth (above).  Bits 29-31 compute the same
- * results; they exist for the separate-process A/Bs recorded in profiles/. */
+ * results; they exist for the separate-process A/Bs recorded in profiles/.
+ * The header row kernel (k_hdr: 20/24-byte strides, no pseudo-header) takes
+ * loads_per_lane 8/16/24/32 = its ring (default 32) and 1 = never k_hdr (k_small
+ * instead), bits 8..15 = its rows per wave task, and reads bits 29-31 as its
+ * result-store policy: 29 = plain write-back, 30 = non-temporal (default
+ * write-through sc1), 31 = one store per result instead of 16-byte pieces. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
 /* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the

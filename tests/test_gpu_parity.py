@@ -181,14 +181,14 @@ def last_kernel() -> str:
 
 
 # the kernel each config's bench launch runs: the fixture pins THAT kernel
-BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
+BENCH_KERNEL = {1: "k_hdr<5,", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
 def test_batch_kernel_reproduces_pips_results(batches, name):
     """pip's own results (compiled pip_checksum.cpp, tests/golden/make_golden.py)
     through the batch kernel and layout the bench runs: cfg1 at the packed 20-B
-    stride (k_small), cfg4 as a packed-lengths batch (k_packed) and, for the
+    stride (k_hdr), cfg4 byte-packed (k_packedb) and 16-B packed (k_packed) and, for the
     descriptor ABI, as ragged descriptors (k_ragged)."""
     b, w = batches[name], ALL[name]
     assert b["stride"] == w.stride
@@ -495,6 +495,47 @@ def test_small_packet_kernel_vs_oracle(oracle, misalign):
         for i in range(0, n, 7):
             s, d = oracle.flow4(99, int(flow_of[i]))
             assert got[i] == oracle.inet_checksum(host[i * 24:i * 24 + L].tobytes(), 6, s, d)
+    finally:
+        engine.tune()
+
+
+@pytest.mark.parametrize("stride", [20, 24])
+@pytest.mark.parametrize("ring,rows", [(0, 0), (8, 1), (16, 3), (24, 64), (16, 128)])
+def test_header_row_kernel_vs_oracle(oracle, stride, ring, rows):
+    """k_hdr (pipck_hdr.hip): packed 20/24-byte items with no pseudo-header
+    (cfg1's IPv4 headers) streamed as rows of whole headers, each header split
+    over two lanes.  Every length up to the stride (bytes past `len` masked,
+    odd lengths), batches ending inside a row, on a row and on a task boundary,
+    all-0xFF / all-zero headers, RX verify; every ring and task size."""
+    rng = np.random.default_rng(700 + stride + ring + rows)
+    engine.tune(0, ring, 0, rows_per_task=rows)
+    try:
+        per = (rows or 64) * (48 if stride == 20 else 42)  # headers per wave task
+        for length in sorted({0, 1, 2, 3, 4, 5, 11, 19, 20, stride - 1, stride}):
+            for n in sorted({1, 47, 48, 49, per - 1, per, per + 1, 4 * per + 7, 20000}):
+                host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
+                if n > 3:
+                    host[stride:2 * stride] = 0xFF
+                    host[2 * stride:3 * stride] = 0
+                _, arena = upload(host, 0)
+                want = oracle.batch_fixed(host, stride, length, n, 0, 0, 0, N_FLOWS, 0)
+                got = u16(engine.checksum_fixed(arena, stride, length, n, None, N_FLOWS, None, 0))
+                assert "k_hdr<" in last_kernel(), last_kernel()
+                assert np.array_equal(got, want), (length, n, np.nonzero(got != want)[0][:5])
+                ok = engine.verify_fixed(arena, stride, length, n, None, N_FLOWS, None, 0).cpu().numpy()
+                assert "k_hdr<" in last_kernel()
+                assert np.array_equal(ok.astype(bool), got == 0)
+        # checksummed IPv4 headers verify; one flipped bit is caught
+        n = 5000
+        host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
+        for i in range(n):
+            host[i * stride + 10:i * stride + 12] = 0
+            c = oracle.ip_checksum(host[i * stride:i * stride + 20].tobytes())
+            host[i * stride + 10], host[i * stride + 11] = c >> 8, c & 0xFF
+        host[17 * stride + 3] ^= 0x10
+        _, arena = upload(host, 0)
+        ok = engine.verify_fixed(arena, stride, 20, n, None, N_FLOWS, None, 0).cpu().numpy().astype(bool)
+        assert not ok[17] and ok.sum() == n - 1
     finally:
         engine.tune()
 
