@@ -290,8 +290,12 @@ int main(int argc, char** argv) {
         Conn& c = g_conns[k];
         g_connecting = (int)k;
         auto syn = craft(c.port, c.cseq, 0, TH_SYN, opts);
+        const double ts = now();
         nif.input(syn.data());
         settle();
+        // the SYN-ACK stays unacknowledged until the ACK below: a stall here past
+        // pip's 1 s timer makes it resend (reported, and the run fails)
+        if (now() - ts > 0.1) fprintf(stderr, "slow handshake: SYN -> SYN-ACK out took %.3f s\n", now() - ts);
         if (!c.tcp) { fprintf(stderr, "no connection %u\n", k); return 1; }
         c.cseq += 1;
         auto ack = craft(c.port, c.cseq, c.srv_next, TH_ACK, {});

@@ -39,12 +39,14 @@ constexpr int coop_waves_per_simd() { return U >= 32 ? 2 : (U >= 24 ? 3 : (U >= 
 
 __host__ __device__ constexpr uint32_t coop_pitch(uint32_t k) { return k | 1u; }  // odd: lanes hit distinct banks
 
-template <int U, bool VERIFY, bool NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void k_flat_coop(
-    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
-    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
-    extern __shared__ uint32_t s_part[];  // 64 lanes x pitch u32 (launch_coop sizes it)
+// The kernel body; PROBE = false compiles the measurement bits out of the
+// production kernel k_flat_coop (no per-row flag test), k_flat_coop_probe keeps them.
+template <int U, bool VERIFY, bool NT, bool PROBE>
+__device__ __forceinline__ void coop_body(uint32_t* s_part, const uint8_t* __restrict__ arena, uint32_t cpp,
+                                          uint32_t len, uint64_t n, uint32_t K, const uint32_t* __restrict__ pseudo,
+                                          uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    if (!PROBE) kflags &= ~(kCoopLoadsOnly | kCoopNoEnd);
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint32_t pitch = coop_pitch(K);
@@ -123,6 +125,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_
     }
 }
 
+template <int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void k_flat_coop(
+    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
+    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint32_t s_part[];  // 64 lanes x pitch u32 (launch_coop sizes it)
+    coop_body<U, VERIFY, NT, false>(s_part, arena, cpp, len, n, K, pseudo, n_flows, flow_of, flow_origin, out, ok,
+                                    kflags);
+}
+
+// k_flat_coop with the measurement bits 21 / 22 live (tools only)
+template <int U, bool VERIFY, bool NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void
+k_flat_coop_probe(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
+                  const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of,
+                  uint64_t flow_origin, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint32_t s_part[];
+    coop_body<U, VERIFY, NT, true>(s_part, arena, cpp, len, n, K, pseudo, n_flows, flow_of, flow_origin, out, ok,
+                                   kflags);
+}
+
 typedef void (*coop_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
                         const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
 
@@ -153,8 +176,11 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
         {k_flat_coop<16, false, true>, k_flat_coop<16, true, true>},
         {k_flat_coop<24, false, true>, k_flat_coop<24, true, true>},
         {k_flat_coop<32, false, true>, k_flat_coop<32, true, true>}};
+    static const coop_fn kCoopProbe[3] = {k_flat_coop_probe<16, false, true>, k_flat_coop_probe<24, false, true>,
+                                          k_flat_coop_probe<32, false, true>};
     const int ui = u >= 32 ? 2 : (u >= 24 ? 1 : 0);
-    PIPCK_LAUNCH(kCoop[ui][verify], dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, len, n,
+    const bool probe = (kflags & (kCoopLoadsOnly | kCoopNoEnd)) && !verify;
+    PIPCK_LAUNCH(probe ? kCoopProbe[ui] : kCoop[ui][verify], dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, len, n,
                  K, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, kflags);
     PIPCK_LAUNCHED("k_flat_coop");
     return PIPCK_OK;

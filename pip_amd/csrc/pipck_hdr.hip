@@ -170,11 +170,10 @@ int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, 
     const uint32_t PR = stride == 20 ? HdrGeom<5>::PR : HdrGeom<6>::PR;
     // rows per wave task: 32 with a ring of 32 (the whole task in flight at
     // once) measured fastest at 128M-256M headers -- 0.979 ms at 256M vs
-    // 0.99-1.08 for 24-48 rows or a ring of 24, and k_small's 1.089
-    // (profiles/r03_hdr_scan.jsonl); smaller batches get shorter tasks so the
-    // grid still holds >= 2,048 waves (4-row steps keep results 16-B aligned)
-    uint32_t R = rows ? std::min<uint32_t>(rows, 128u) : 32u;  // LDS: 4 x R x PR results
-    if (!rows) R = (uint32_t)std::max<uint64_t>(4u, std::min<uint64_t>(R, n / (2048ull * PR)) / 4u * 4u);
+    // 0.99-1.08 for 24-48 rows or a ring of 24, and k_small's 1.089 -- and
+    // shorter tasks were slower at every size down to 1M headers
+    // (profiles/r03_hdr_scan.jsonl)
+    const uint32_t R = rows ? std::min<uint32_t>(rows, 128u) : 32u;  // LDS: 4 x R x PR results
     const uint64_t per = (uint64_t)R * PR;
     const uint64_t tasks = (n + per - 1) / per;
     const uint64_t blocks = (tasks + 3) / 4;

@@ -485,12 +485,15 @@ __device__ __forceinline__ void flat_reduce_rows(const u32x4 (&v)[U], uint32_t r
 template <int U>
 constexpr int flat_waves_per_simd() { return U >= 32 ? 2 : (U >= 24 ? 3 : (U >= 16 ? 4 : (U >= 8 ? 5 : 6))); }
 
-template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n,
-                                              uint32_t run, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
-                                              const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
-    extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16 (launch_fixed sizes it)
+// The kernel body; PROBE = false compiles the measurement-only bits (21-23)
+// out of the production kernel k_flat (no per-row flag test), and k_flat_probe
+// keeps them for the tools.
+template <int U, bool PIPE, bool VERIFY, bool NT, int WPB, bool PROBE>
+__device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __restrict__ arena, uint32_t cpp,
+                                          uint32_t len, uint64_t n, uint32_t run, const uint32_t* __restrict__ pseudo,
+                                          uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    if (!PROBE) kflags &= ~(kLoadsOnly | kNoTaskEnd | kEndNoStore);
     const int lane = threadIdx.x & 63;
     const uint32_t pitch = flat_pitch(run);
     uint16_t* part = s_part + (threadIdx.x >> 6) * 64u * pitch;
@@ -610,6 +613,27 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
         trace_task(kflags, trb, task, t_start, lane);
         wave_sync();
     }
+}
+
+template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(
+    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
+    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16 (launch_fixed sizes it)
+    flat_body<U, PIPE, VERIFY, NT, WPB, false>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of, flow_origin,
+                                               out, ok, kflags);
+}
+
+// k_flat with the measurement bits 21-23 live (tools only)
+template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_probe(
+    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
+    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint16_t s_part[];
+    flat_body<U, PIPE, VERIFY, NT, WPB, true>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of, flow_origin,
+                                              out, ok, kflags);
 }
 
 // ---------------------------------------------------------------------------
@@ -1416,7 +1440,8 @@ static const SmallVariant& small_variant() {
     return kSmall[k >= 1 && k <= 4 ? k - 1 : 0];
 }
 
-constexpr uint32_t kNoFlatSmall = 128u;  // pipck_tune flags bit 7: never the short-stride flat kernel
+constexpr uint32_t kNoFlatSmall = 128u;
+constexpr uint64_t kHdrMinBatch = 8ull << 20;  // headers: k_hdr from here, k_small below  // pipck_tune flags bit 7: never the short-stride flat kernel
 
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
@@ -1426,13 +1451,14 @@ struct FlatVariant {
     int u;
     bool pipe;
     flat_fn fn[2][2];  // [verify][nt]
+    flat_fn probe;     // k_flat_probe (checksum, nt loads) for the default rings, else null
 };
 #define PIPCK_F(U, P)                                                                     \
     {                                                                                     \
         U, P, {                                                                           \
             {k_flat<U, P, false, false>, k_flat<U, P, false, true>},                      \
             {k_flat<U, P, true, false>, k_flat<U, P, true, true>}                         \
-        }                                                                                 \
+        }, (P && (U == 24 || U == 32)) ? k_flat_probe<U, P, false, true> : nullptr        \
     }
 // loads_per_lane 2/4/8/16 = U rows in flight per wave; 3/5/9/13/17/25/33 = ring-pipelined U = 2/4/8/12/16/24/32
 // (a ring of 40 or 48 -- 231 / 272 VGPRs -- ran cfg5 1 % / 28 % slower than 32,
@@ -1549,7 +1575,9 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint32_t grid = grid_for(4, tasks, 0);
         // per-wave partials + the block's results + its completion counter
         const size_t lds = (4u * 64u * flat_pitch(run) + ((4u * run + 1u) & ~1u)) * sizeof(uint16_t) + 16u;
-        PIPCK_LAUNCH(fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
+        // the measurement bits (21-23) run k_flat_probe; the production kernel has them compiled out
+        const bool probe = (flags & (kLoadsOnly | kNoTaskEnd | kEndNoStore)) && fv->probe && !verify && nt_for(true);
+        PIPCK_LAUNCH(probe ? fv->probe : fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
         PIPCK_LAUNCHED("k_flat");
@@ -1573,12 +1601,19 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         return PIPCK_OK;
     }
     // Packed 20/24-byte items with no pseudo-header (IPv4 headers, cfg1): rows
-    // of whole headers streamed like the large-packet kernels (pipck_hdr.hip).
-    // pipck_tune loads_per_lane 8/16/24/32 = its ring, 1 = never (k_small instead).
-    if (!d_pseudo && (stride == 20 || stride == 24) && !g_tune.lanes.load() && g_tune.loads.load() != 1) {
+    // of whole headers streamed like the large-packet kernels (pipck_hdr.hip),
+    // from 8M headers up: 8.6 % faster than k_small at 256M, 6-11 % at 16M-64M,
+    // even at 8M, and slower below (1M: 15.3 vs 12.0 us) where k_small's many
+    // tiny waves fill the chip sooner (profiles/r03_hdr_scan.jsonl).
+    // pipck_tune loads_per_lane 8/16/24/32 = k_hdr with that ring at any size,
+    // 1 = never k_hdr.
+    {
         const uint32_t lq = g_tune.loads.load(), flags = g_tune.flags.load();
-        if (launch_hdr(verify, d_arena, stride, len, n, d_out, d_ok, as_stream(stream), (flags >> 8) & 0xFFu,
-                       lq == 8 || lq == 16 || lq == 24 || lq == 32 ? lq : 0u, nt_for(true), flags) == PIPCK_OK)
+        const bool force = lq == 8 || lq == 16 || lq == 24 || lq == 32;
+        if (!d_pseudo && (stride == 20 || stride == 24) && !g_tune.lanes.load() && lq != 1 &&
+            (force || n >= kHdrMinBatch) &&
+            launch_hdr(verify, d_arena, stride, len, n, d_out, d_ok, as_stream(stream), (flags >> 8) & 0xFFu,
+                       force ? lq : 0u, nt_for(true), flags) == PIPCK_OK)
             return PIPCK_OK;
     }
     // Tiny 8-B-multiple strides with pseudo-headers (pure ACKs, small UDP) or

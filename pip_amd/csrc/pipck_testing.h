@@ -43,6 +43,9 @@ extern "C" {
  * alone).  Bit 22 = MEASUREMENT ONLY, NO RESULTS: k_flat skips its task end.
  * Bit 23 = MEASUREMENT ONLY, NO RESULTS: k_flat computes its results but stores
  * none (bits 21-23 isolate the task-end cost, profiles/r03_flat_end_probe.jsonl).
+ * Bits 21-23 launch separate probe kernels (k_flat_probe, k_flat_coop_probe:
+ * checksum mode, non-temporal loads, rings 24/32 for k_flat); the production
+ * kernels have them compiled out and ignore them otherwise.
  * Bit 28 = the other fixed-stride schedule: k_flat for jumbo strides (default
  * there: the block-cooperative k_flat_coop), k_flat_coop for shorter ones
  * (default there: k_flat); for k_flat_coop, bits 8..15 are rows per wave and

@@ -174,7 +174,7 @@ def sha(a) -> str:
 EDGES = {
     "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat<24,"},
     "edge_flat32_udp6": {"cfg": 3, "n": 48, "ck_every": 2, "ck_off": 6, "kernel": "k_flat_coop<32,"},
-    "edge_small_ip20": {"cfg": 1, "n": 4096, "ck_every": 5, "ck_off": 10, "zero_every": 7, "kernel": "k_hdr<5,"},
+    "edge_small_ip20": {"cfg": 1, "n": 4096, "ck_every": 5, "ck_off": 10, "zero_every": 7, "kernel": "k_small<"},
     "edge_packed_tcp4": {"cfg": 4, "n": 4096, "ck_every": 2, "ck_off": 16, "zero_every": 0, "kernel": "k_packed<"},
     "edge_packedb_tcp4": {"cfg": 4, "n": 4096, "ck_every": 3, "ck_off": 16, "zero_every": 0, "layout": "bytes",
                           "kernel": "k_packedb<"},

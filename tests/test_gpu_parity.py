@@ -181,14 +181,14 @@ def last_kernel() -> str:
 
 
 # the kernel each config's bench launch runs: the fixture pins THAT kernel
-BENCH_KERNEL = {1: "k_hdr<5,", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
+BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
 def test_batch_kernel_reproduces_pips_results(batches, name):
     """pip's own results (compiled pip_checksum.cpp, tests/golden/make_golden.py)
     through the batch kernel and layout the bench runs: cfg1 at the packed 20-B
-    stride (k_hdr), cfg4 byte-packed (k_packedb) and 16-B packed (k_packed) and, for the
+    stride (k_small at the config's 1M; k_hdr from 8M), cfg4 byte-packed (k_packedb) and 16-B packed (k_packed) and, for the
     descriptor ABI, as ragged descriptors (k_ragged)."""
     b, w = batches[name], ALL[name]
     assert b["stride"] == w.stride
@@ -209,6 +209,14 @@ def test_batch_kernel_reproduces_pips_results(batches, name):
         outs = {"fixed": engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None,
                                                b["first"])}
         kernel = last_kernel()
+        if w.cfg == 1:  # the header row kernel that batches of >= 8M headers take (k_hdr)
+            engine.tune(loads_per_lane=32)
+            try:
+                outs["hdr"] = engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None,
+                                                    b["first"])
+                assert "k_hdr<5," in last_kernel()
+            finally:
+                engine.tune()
     assert BENCH_KERNEL[w.cfg] in kernel, kernel
     for path, out in outs.items():
         got = u16(out)
@@ -255,10 +263,19 @@ def test_edge_fixture_through_batch_kernel(batches, name):
     else:
         out = engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None, b["first"])
     assert b["kernel"] in last_kernel(), last_kernel()
-    got = u16(out)
-    assert int((got == 0).sum()) == b["n_zero"] and int((got == 0xFFFF).sum()) == b["n_ffff"]
-    assert list(got[:16]) == b["head"]
-    assert sha(got.astype("<u2")) == b["results_sha256"]
+    outs = [out]
+    if b["kernel"] == "k_small<" and not fam:  # IPv4 headers: also through k_hdr (batches >= 8M headers)
+        engine.tune(loads_per_lane=32)
+        try:
+            outs.append(engine.checksum_fixed(arena, b["stride"], b["length"], n, None, b["n_flows"], None, b["first"]))
+            assert "k_hdr<" in last_kernel()
+        finally:
+            engine.tune()
+    for out in outs:
+        got = u16(out)
+        assert int((got == 0).sum()) == b["n_zero"] and int((got == 0xFFFF).sum()) == b["n_ffff"]
+        assert list(got[:16]) == b["head"]
+        assert sha(got.astype("<u2")) == b["results_sha256"]
 
 
 @pytest.mark.parametrize("small_k_log", [0, 1, 2, 3, 4])
@@ -500,7 +517,7 @@ def test_small_packet_kernel_vs_oracle(oracle, misalign):
 
 
 @pytest.mark.parametrize("stride", [20, 24])
-@pytest.mark.parametrize("ring,rows", [(0, 0), (8, 1), (16, 3), (24, 64), (16, 128)])
+@pytest.mark.parametrize("ring,rows", [(32, 0), (8, 1), (16, 3), (24, 64), (16, 128)])
 def test_header_row_kernel_vs_oracle(oracle, stride, ring, rows):
     """k_hdr (pipck_hdr.hip): packed 20/24-byte items with no pseudo-header
     (cfg1's IPv4 headers) streamed as rows of whole headers, each header split
@@ -971,16 +988,19 @@ def test_generator_is_shard_invariant():
 # ----------------------------------------------------------------------------
 # 8. full BASELINE.json sizes: sampled oracle comparison + checksum-of-checksum
 # ----------------------------------------------------------------------------
-FULL = [(CFG1, 1 << 20, 0), (CFG2, 4 << 20, 0), (CFG3, 1 << 20, 0), (CFG5, 8 << 20, 8 << 20)]
+# cfg1 also at 256M headers: the size the f3 line is profiled at, where k_hdr runs
+FULL = [(CFG1, 1 << 20, 0), (CFG1, 256 << 20, 3), (CFG2, 4 << 20, 0), (CFG3, 1 << 20, 0), (CFG5, 8 << 20, 8 << 20)]
 FIELD = {1: 10, 2: 16, 3: 6, 4: 16, 5: 16}  # ip_sum / th_sum / uh_sum offsets
 
 
-@pytest.mark.parametrize("w,n,first", FULL, ids=[w.name for w, _, _ in FULL])
+@pytest.mark.parametrize("w,n,first", FULL, ids=[f"{w.name}_{n}" for w, n, _ in FULL])
 def test_full_size_fixed(oracle, w, n, first):
     arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
     engine.gen_fixed(arena, w.stride, w.length, n, first, w.seed, w.hdr)
     pseudo = _pseudo(w)
     out = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, first)
+    if w.cfg == 1:
+        assert ("k_hdr<5," if n >= 8 << 20 else "k_small<") in last_kernel()
     got = u16(out)
     rng = np.random.default_rng(w.cfg)
     for i in rng.choice(n, 1500, replace=False):

@@ -102,7 +102,7 @@ def test_edge_fixtures_cover_both_corners(batches):
     assert any(b["family"] and b["n_ffff"] for b in edges)
     # and 0x0000 through every batch kernel family the bench runs
     kernels = {b["kernel"] for b in edges if b["n_zero"]}
-    assert {"k_flat<24,", "k_flat_coop<32,", "k_hdr<5,", "k_packed<", "k_packedb<"} <= kernels
+    assert {"k_flat<24,", "k_flat_coop<32,", "k_small<", "k_packed<", "k_packedb<"} <= kernels
 
 
 def test_zipf_shape(oracle):
