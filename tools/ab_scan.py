@@ -2,7 +2,7 @@
 """A/B of libpipck builds on one GPU box (box-to-box variation is a few %,
 larger than most kernel changes).
 
-    python tools/ab_scan.py [--only cfg2,cfg4] [--rounds 3] pip_amd/lib/ab/libpipck_base.so [more.so ...]
+    python tools/ab_scan.py [--only cfg2,cfg4] [--rounds 3] pip_amd/lib/ab/libpipck_base.so [more.so ...] [cur@1024]
 
 Each given library is an arm named after its file stem (minus "libpipck_"),
 arm "cur" = pip_amd/lib/libpipck.so.  Every (round, arm) runs in its OWN
@@ -38,6 +38,9 @@ def worker(only: list[str], iters: int) -> None:
     from size_scan import timed
 
     engine.require_gpu()
+    # placement probe: PIPCK_AB_PAD_MB of device memory held before the batches
+    # are allocated, so the same build's arena lands elsewhere in HBM
+    pad = torch.empty(int(os.environ.get("PIPCK_AB_PAD_MB", "0")) << 20, dtype=torch.uint8, device="cuda")
     for name in only:
         w, n = BY_CFG[int(name[3:4])], WORKLOADS[name]
         fam = w.family or (4 if name.endswith("p") else 0)  # cfg1p: cfg1 with IPv4 pseudo-headers
@@ -76,14 +79,21 @@ def main():
     if a.worker:
         worker(only, a.iters)
         return
-    arms = {Path(x).stem.replace("libpipck_", ""): str(Path(x).resolve()) for x in a.libs}
-    arms["cur"] = str(ROOT / "pip_amd" / "lib" / "libpipck.so")
+    # an arm is a library path, or "path@MB" / "cur@MB": that build with MB of
+    # device memory allocated before its batches (a placement probe)
+    arms = {}
+    for x in a.libs:
+        lib, _, pad = x.partition("@")
+        path = ROOT / "pip_amd" / "lib" / "libpipck.so" if lib == "cur" else Path(lib).resolve()
+        name = "cur" if lib == "cur" else Path(lib).stem.replace("libpipck_", "")
+        arms[name + (f"_pad{pad}" if pad else "")] = (str(path), pad or "0")
+    arms.setdefault("cur", (str(ROOT / "pip_amd" / "lib" / "libpipck.so"), "0"))
     res: dict[tuple[str, str], list[float]] = {}
     meta: dict[str, dict] = {}
     for rnd in range(a.rounds):
         order = list(arms.items()) if rnd % 2 == 0 else list(reversed(arms.items()))
-        for arm, path in order:
-            env = dict(os.environ, PIPCK_LIB=path)
+        for arm, (path, pad) in order:
+            env = dict(os.environ, PIPCK_LIB=path, PIPCK_AB_PAD_MB=pad)
             r = subprocess.run([sys.executable, __file__, "--worker", "--only", ",".join(only), "--iters",
                                 str(a.iters)], env=env, capture_output=True, text=True, timeout=600)
             if r.returncode:
