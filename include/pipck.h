@@ -82,7 +82,11 @@ int pipck_flows6_prepare(const pipck_flow6* d_flows, uint32_t n_flows, uint32_t*
  * which equals pip_inet_checksum / pip_inet6_checksum (pip_checksum.cpp:42-87)
  * and pip_inet{,6}_checksum_buf on a single-segment chain (:90-148).        */
 
-/* Fixed stride: packet i = d_arena + i*stride, len bytes.  Any alignment. */
+/* Fixed stride: packet i = d_arena + i*stride, len bytes.  Any alignment.
+ * The kernels load whole aligned 16-byte chunks, so the bytes from the 16-byte
+ * boundary at or below d_arena to the one at or above the last packet's end
+ * must be readable device memory (every hipMalloc / torch allocation is: they
+ * are 256-byte granular); bytes outside the packets never affect a result. */
 int pipck_checksum_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
                          const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                          uint64_t flow_origin, uint16_t* d_out, void* stream);
