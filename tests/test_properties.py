@@ -12,7 +12,9 @@ CPU only.  Three independent statements are compared on random inputs:
   u64, bytes outside the segment masked, one byte swap for a segment that
   starts at an even address, residue-and-zero-preserving folds.
 
-plus pip-level invariants: a stored checksum makes the packet verify, and
+and ``hdr_row_emulation`` -- the IPv4-header row kernel's split of each
+20/24-byte item over two lanes (pip_amd/csrc/pipck_hdr.hip) -- against pip's
+ip checksum; plus pip-level invariants: a stored checksum makes the packet verify, and
 RFC 1624's incremental update equals recomputation except at the 0x0000 /
 0xFFFF corner the kernel settles by rescanning.
 """
@@ -163,3 +165,58 @@ def test_rfc1624_update_equals_recompute(data, new, proto, src, dst):
         assert upd == want
     else:  # pip gives 0x0000 for a nonzero sum and 0xFFFF for an all-zero one
         assert want in (0x0000, 0xFFFF)
+
+
+def hdr_row_emulation(mem: bytes, D: int, length: int, n: int) -> list[int]:
+    """k_hdr's method (pip_amd/csrc/pipck_hdr.hip) restated per lane: rows of
+    C = 60 (D = 5) or 63 (D = 6) 16-byte chunks hold whole 4*D-byte items; lane l
+    splits its chunk's dwords into H (the item begun in an earlier lane) and T
+    (the item beginning in it) with bytes past `length` masked; the lane holding
+    an item's last dword finishes it from T of the lane before plus its own H.
+    dot4 = lo16 + hi16 of every masked dword (v_dot2_u32_u16 against (1, 1))."""
+    C = 60 if D == 5 else 63
+    PR = C * 4 // D
+    masks_h, masks_t, fin = [], [], []
+    for lane in range(64):
+        h, t, start, f = [0] * 4, [0] * 4, 4, -1
+        for i in range(4):
+            d = 4 * lane + i
+            q = d % D
+            if q == 0 and start == 4:
+                start = i
+            if q == D - 1:
+                f = d // D
+            vb = length - 4 * q
+            m = 0xFFFFFFFF if vb >= 4 else (0 if vb <= 0 else (0xFFFFFFFF >> (32 - 8 * vb)))
+            h[i], t[i] = (m, 0) if i < start else (0, m)
+        if lane >= C:
+            h, t, f = [0] * 4, [0] * 4, -1
+        masks_h.append(h), masks_t.append(t), fin.append(f)
+    out = [None] * n
+    rows = (n + PR - 1) // PR
+    for r in range(rows):
+        T = [0] * 64
+        H = [0] * 64
+        for lane in range(C):
+            off = 16 * (C * r + lane)
+            dw = [int.from_bytes(mem[off + 4 * i:off + 4 * i + 4].ljust(4, b"\0"), "little") for i in range(4)]
+            H[lane] = sum((x & m & 0xFFFF) + ((x & m) >> 16) for x, m in zip(dw, masks_h[lane]))
+            T[lane] = sum((x & m & 0xFFFF) + ((x & m) >> 16) for x, m in zip(dw, masks_t[lane]))
+        for lane in range(64):
+            hi = r * PR + fin[lane]
+            if fin[lane] >= 0 and hi < n:
+                s = (T[lane - 1] if lane else 0) + H[lane]
+                w = fold(fold(s))
+                out[hi] = ~(((w & 0xFF) << 8) | (w >> 8)) & 0xFFFF  # even starts: byte swap, then pip's ~
+    return out
+
+
+@settings(max_examples=60, deadline=None)
+@given(stride=st.sampled_from([20, 24]), data=st.data(), n=st.integers(1, 130))
+def test_header_row_split_equals_pips_ip_checksum(stride, data, n):
+    """Every item of a packed 20/24-byte batch, split over two lanes as k_hdr
+    splits it, gets pip_ip_checksum of its first `length` bytes."""
+    length = data.draw(st.integers(0, stride))
+    mem = data.draw(st.binary(min_size=n * stride, max_size=n * stride)) + bytes(1024)
+    got = hdr_row_emulation(mem, stride // 4, length, n)
+    assert got == [py_ip(mem[i * stride:i * stride + length]) for i in range(n)]
