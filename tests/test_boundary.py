@@ -95,3 +95,31 @@ def test_pip_tx_path_at_volume_matches_pip(mss):
             modes.append(("--mode", "capture_zc", "--pipeline"))
         for m in modes:
             assert run(amd_bin, "--conns", conns, *m) == want, (conns, m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family,length", [(6, 8952), (4, 8972), (4, 1472)])
+def test_pip_udp_tx_path_matches_pip(family, length):
+    """pip's UDP send path (pip_udp::output, pip/protocol/pip_udp.cpp:28-64) at
+    volume through oracle/stack_udp_bench.cpp: pip's own build vs the drop-in
+    synchronously, in capture mode, with zero-copy and pipelined batches --
+    FNV-1a over every emitted wire byte must be identical."""
+    import json
+
+    ref_bin = ROOT / "oracle" / "_ref" / "stack_udp_ref"
+    amd_bin = ROOT / "oracle" / "_ref" / "stack_udp_amd"
+    assert ref_bin.exists() and amd_bin.exists(), "build with `make -C oracle ref ref-amd`"
+
+    def run(binary, nbytes, *args):
+        r = subprocess.run([str(binary), "--family", str(family), "--len", str(length), "--bytes", str(nbytes),
+                            "--verify", *args], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (args, r.stderr[-2000:])
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["digest_of"] == "every wire byte" and d["datagrams"] == nbytes // length
+        return d["digest"]
+
+    assert run(amd_bin, 4 << 20, "--mode", "sync") == run(ref_bin, 4 << 20)
+    want = run(ref_bin, 16 << 20)
+    for args in (("--mode", "capture"), ("--mode", "capture_zc"), ("--mode", "capture_zc", "--pipeline"),
+                 ("--mode", "capture_zc", "--pipeline", "--batch", "1000")):
+        assert run(amd_bin, 16 << 20, *args) == want, args
