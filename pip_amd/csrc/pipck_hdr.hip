@@ -125,7 +125,9 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
     const uint32_t rbytes = VERIFY ? np : 2u * np;
     const buf_t rb = VERIFY ? buf_rsrc(ok + p0, np) : buf_rsrc(out + p0, 2u * np);
     uint32_t done = 0;
-    if (!(kflags & kHdrNarrowStores) && (p0 * (VERIFY ? 1u : 2u)) % 16 == 0) {
+    // (16-byte pieces only where the caller's result array is 16-byte aligned there)
+    if (!(kflags & kHdrNarrowStores) &&
+        (VERIFY ? (uintptr_t)(ok + p0) : (uintptr_t)(out + p0)) % 16 == 0) {
         done = rbytes & ~15u;
         const uint32_t per_piece = VERIFY ? 16u : 8u;  // results per 16 bytes
         for (uint32_t o = 16u * lane; o < done; o += 1024u) {

@@ -542,6 +542,22 @@ def test_header_row_kernel_vs_oracle(oracle, stride, ring, rows):
                 ok = engine.verify_fixed(arena, stride, length, n, None, N_FLOWS, None, 0).cpu().numpy()
                 assert "k_hdr<" in last_kernel()
                 assert np.array_equal(ok.astype(bool), got == 0)
+        # result arrays at every 2-byte / 1-byte offset from a 16-byte boundary (the
+        # kernel writes 16-byte pieces only where the caller's array is aligned)
+        n = 5000
+        host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
+        _, arena = upload(host, 0)
+        want = oracle.batch_fixed(host, stride, 20, n, 0, 0, 0, N_FLOWS, 0)
+        for shift in range(8):
+            buf = torch.zeros(n + 16, dtype=torch.int16, device=DEV)
+            got = u16(engine.checksum_fixed(arena, stride, 20, n, None, N_FLOWS, None, 0, out=buf[shift:shift + n]))
+            assert np.array_equal(got, want), shift
+            assert not buf[:shift].any() and not buf[shift + n:].any(), shift  # nothing written outside
+        okbuf = torch.zeros(n + 32, dtype=torch.uint8, device=DEV)
+        for shift in (0, 1, 5, 15):
+            okbuf.zero_()
+            ok = engine.verify_fixed(arena, stride, 20, n, None, N_FLOWS, None, 0, ok=okbuf[shift:shift + n])
+            assert np.array_equal(ok.cpu().numpy().astype(bool), want == 0) and not okbuf[:shift].any(), shift
         # checksummed IPv4 headers verify; one flipped bit is caught
         n = 5000
         host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
