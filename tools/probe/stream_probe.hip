@@ -223,7 +223,7 @@ static void run(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out, ui
 #define PROBE_CASE(u, w) \
     if (m.U == u && m.WPB == w) return launch<u, w>(m, a, rows, out, ctr, cus);
     PROBE_CASE(16, 4) PROBE_CASE(24, 4) PROBE_CASE(32, 4) PROBE_CASE(24, 1) PROBE_CASE(24, 2) PROBE_CASE(24, 8)
-    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12)
+    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8)
     fprintf(stderr, "no instance U=%d WPB=%d\n", m.U, m.WPB);
     exit(2);
 }
@@ -240,6 +240,9 @@ int main(int argc, char** argv) {
         {"coop_u24_w4_t64_ovh48", 24, 4, 64, 4}, {"coop_u24_w4_t64_g2", 24, 4, 64, 12}, {"coop_u24_w4_t64_g4", 24, 4, 64, 14},
         {"coop_u24_w4_t64_g8", 24, 4, 64, 18}, {"coop_u24_w4_t64_g16", 24, 4, 64, 26},
         {"coop_persist_u24_t64", 24, 4, 64, 5}, {"coop_persist_u24_t16", 24, 4, 16, 5}, {"coop_persist_u16_t64", 16, 4, 64, 5}, {"coop_u16_w4_t64_ovh24", 16, 4, 64, 3}, {"coop_u16_w4_t64_ovh48", 16, 4, 64, 4},
+        // wider blocks: 8 / 16 waves interleaved row by row over one block task
+        {"coop_u24_w8_t64", 24, 8, 64, 1}, {"coop_u32_w8_t64", 32, 8, 64, 1}, {"coop_u16_w16_t64", 16, 16, 64, 1},
+        {"coop_u16_w8_t64", 16, 8, 64, 1}, {"coop_u24_w8_t32", 24, 8, 32, 1},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";
