@@ -95,4 +95,17 @@ void pip_checksum_amd_resident(bool on);
 void pip_checksum_amd_capture(bool on);
 bool pip_checksum_amd_capturing();
 
+// ---- RX batch verification (pip itself never verifies) ----
+// Verify n received IP packets (as read from the tun device: IPv4 or IPv6,
+// pkts[i] of lens[i] bytes) in one GPU batch on this thread.  ok[i] bit 0 =
+// the IPv4 header checksum verifies (always set for IPv6), bit 1 = the TCP or
+// UDP checksum over its pseudo-header verifies (also set when the packet
+// carries none this verifies: another protocol, or UDP over IPv4 with a zero
+// checksum, RFC 768); ok[i] == 3 = accept.  A malformed packet (lengths that do
+// not fit, not IPv4/IPv6) gets 0.  Packets in pinned memory are read in place;
+// the call returns when every result is known.  Returns the number of packets
+// with ok == 3.  Uses its own queue: pip's deferred TX batch is not touched.
+extern "C" uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n,
+                                                    uint8_t* ok);
+
 #endif

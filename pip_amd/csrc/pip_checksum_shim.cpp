@@ -245,4 +245,95 @@ void pip_checksum_amd_resident(bool on) {
 
 void pip_checksum_amd_capture(bool on) { t_ctx.capture = on; }
 
+// ---- RX batch verification ------------------------
+// pip never checks a received checksum (pip/pip_netif.cpp:45-77,
+// pip/protocol/pip_tcp_input.cpp, pip/protocol/pip_udp.cpp:11-26).  Received
+// packets go through a second per-thread queue (pip's TX queue is left alone):
+// each IPv4 header and each TCP / UDP segment is queued with its stored
+// checksum INCLUDED, so pip's arithmetic yields 0x0000 exactly for a packet
+// that verifies, and the queue stores that result into a scratch word.
+namespace {
+
+struct RxCtx {
+    pipck_txq* q = nullptr;
+    ~RxCtx() {
+        if (q) pipck_txq_destroy(q);
+    }
+};
+thread_local RxCtx t_rx;  // first used after t_ctx, so destroyed before it
+
+pipck_txq* rx_queue() {
+    if (!t_rx.q) {
+        int rc = pipck_txq_create(t_ctx.get(), &t_rx.q);
+        if (rc) die("pipck_txq_create", rc);
+        // packets already in pinned memory (a registered tun read ring) are read in place
+        rc = pipck_txq_auto_zero_copy(t_rx.q, 1);
+        if (rc) die("pipck_txq_auto_zero_copy", rc);
+    }
+    return t_rx.q;
+}
+
+uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
+
+}  // namespace
+
+uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n, uint8_t* ok) {
+    if (!n) return 0;
+    if (!pkts || !lens || !ok) die("pip_checksum_amd_verify_packets: null argument", PIPCK_EINVAL);
+    std::vector<uint16_t> ip_res(n, 0xFFFFu), l4_res(n, 0xFFFFu);  // htons(result) lands here; 0 = verified
+    std::vector<uint8_t> queued(n, 0);                              // bit 0: IP header queued, bit 1: segment
+    pipck_txq* q = rx_queue();
+    for (uint32_t i = 0; i < n; i++) {
+        ok[i] = 0;
+        const uint8_t* b = (const uint8_t*)pkts[i];
+        const uint32_t len = lens[i];
+        if (!b || len < 20) continue;
+        const uint8_t* l4 = nullptr;
+        uint32_t l4len = 0;
+        uint8_t proto = 0;
+        int rc = 0;
+        if ((b[0] >> 4) == 4) {
+            const uint32_t ihl = (b[0] & 15u) * 4u, total = rd16(b + 2);
+            if (ihl < 20 || total < ihl || total > len) continue;  // malformed: 0
+            rc = pipck_txq_add_ip(q, b, ihl, &ip_res[i]);          // the header with its ip_sum
+            if (rc) die("pipck_txq_add_ip", rc);
+            queued[i] |= 1;
+            proto = b[9], l4 = b + ihl, l4len = total - ihl;
+        } else if ((b[0] >> 4) == 6 && len >= 40) {
+            const uint32_t plen = rd16(b + 4);
+            if (40 + plen > len) continue;
+            ok[i] |= 1;  // IPv6 has no header checksum
+            proto = b[6], l4 = b + 40, l4len = plen;  // TCP / UDP directly after the fixed header
+        } else {
+            continue;
+        }
+        if ((proto != IPPROTO_TCP && proto != IPPROTO_UDP)) {
+            ok[i] |= 2;  // no checksum this helper verifies (ICMP, extension headers, ...)
+            continue;
+        }
+        if (l4len < (proto == IPPROTO_TCP ? 20u : 8u)) continue;    // truncated segment: bit 1 stays clear
+        if (proto == IPPROTO_UDP && (b[0] >> 4) == 4 && !l4[6] && !l4[7]) {
+            ok[i] |= 2;  // UDP over IPv4 without a checksum (RFC 768)
+            continue;
+        }
+        const pipck_hseg seg{l4, l4len};
+        uint32_t src = 0, dst = 0;  // network order, as in struct in_addr
+        std::memcpy(&src, b + 12, 4);
+        std::memcpy(&dst, b + 16, 4);
+        rc = (b[0] >> 4) == 4 ? pipck_txq_add4(q, &seg, 1, proto, src, dst, &l4_res[i])
+                              : pipck_txq_add6(q, &seg, 1, proto, b + 8, b + 24, &l4_res[i]);
+        if (rc) die("pipck_txq_add", rc);
+        queued[i] |= 2;
+    }
+    int rc = pipck_txq_flush(q);
+    if (rc) die("pipck_txq_flush", rc);
+    uint32_t good = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((queued[i] & 1) && ip_res[i] == 0) ok[i] |= 1;
+        if ((queued[i] & 2) && l4_res[i] == 0) ok[i] |= 2;
+        good += ok[i] == 3;
+    }
+    return good;
+}
+
 bool pip_checksum_amd_capturing() { return t_ctx.capture; }

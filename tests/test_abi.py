@@ -99,6 +99,8 @@ def test_kernels_are_built_for_gfx950_only():
 def test_shim_exports_pip_mangled_names():
     syms = dynsyms(_lib.LIBSHIM)
     assert set(PIP_MANGLED) <= syms
+    # the RX batch verifier is extern "C" (include/pip_checksum_amd.h)
+    assert "pip_checksum_amd_verify_packets" in syms
     needed = subprocess.run(["readelf", "-d", str(_lib.LIBSHIM)], check=True, capture_output=True, text=True).stdout
     assert "libpipck.so" in needed
 

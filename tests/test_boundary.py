@@ -123,3 +123,115 @@ def test_pip_udp_tx_path_matches_pip(family, length):
     for args in (("--mode", "capture"), ("--mode", "capture_zc"), ("--mode", "capture_zc", "--pipeline"),
                  ("--mode", "capture_zc", "--pipeline", "--batch", "1000")):
         assert run(amd_bin, 16 << 20, *args) == want, args
+
+
+def _verify(packets):
+    """pip_checksum_amd_verify_packets (the drop-in's RX batch verifier) over Python bytes."""
+    import ctypes as C
+
+    import numpy as np
+
+    from pip_amd import _lib
+
+    lib = C.CDLL(str(_lib.LIBSHIM))
+    fn = lib.pip_checksum_amd_verify_packets
+    fn.restype = C.c_uint32
+    fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p]
+    bufs = [C.create_string_buffer(bytes(p), max(len(p), 1)) for p in packets]
+    ptrs = (C.c_void_p * len(packets))(*[C.cast(b, C.c_void_p) for b in bufs])
+    lens = (C.c_uint32 * len(packets))(*[len(p) for p in packets])
+    ok = np.zeros(len(packets), dtype=np.uint8)
+    good = fn(ptrs, lens, len(packets), ok.ctypes.data)
+    assert good == int((ok == 3).sum())
+    return ok
+
+
+@pytest.mark.gpu
+def test_rx_verify_accepts_what_pip_emits_and_rejects_corruption():
+    """SURVEY 8 f2 on pip's own packets: every IPv4/IPv6 TCP/UDP packet pip's
+    real stack emits (tests/golden/stack_replay.txt, pip's build) verifies in
+    one GPU batch; flipping any one byte of a packet's IPv4 header or TCP/UDP
+    segment is caught in the right bit; truncated or non-IP packets get 0."""
+    import random
+
+    import numpy as np
+
+    pkts = [bytes.fromhex(l.strip()) for l in GOLDEN.read_text().splitlines() if l.strip() and
+            not l.startswith(("PACKETS", "VERIFY"))]
+    assert len(pkts) >= 20
+    assert (_verify(pkts) == 3).all()
+    rng = random.Random(7)
+    bad, where = [], []
+    for p in pkts:
+        v4 = p[0] >> 4 == 4
+        hl = (p[0] & 15) * 4 if v4 else 40
+        # a byte of the IPv4 header that only its own checksum covers (TOS, id, fragment,
+        # TTL, the checksum itself), or a byte of the TCP/UDP segment
+        i = rng.choice([1, 4, 5, 6, 7, 8, 10, 11] if v4 and rng.random() < 0.5 else list(range(hl, len(p))))
+        q = bytearray(p)
+        q[i] ^= 0x10
+        bad.append(bytes(q))
+        where.append(1 if i < hl else 2)
+    ok = _verify(bad)
+    for o, w in zip(ok, where):
+        assert o == 3 - w, (o, w)  # exactly the damaged checksum fails
+    junk = [b"", bytes(10), bytes([0x45]) + bytes(10), bytes([0x45, 0, 0xFF, 0xFF]) + bytes(16), bytes([0x60]) + bytes(20)]
+    assert (_verify(junk) == 0).all()
+
+
+@pytest.mark.gpu
+def test_rx_verify_against_the_oracle(oracle):
+    """Random TCP/UDP over IPv4 and IPv6 packets whose checksums the oracle
+    (pip's arithmetic) filled in -- odd lengths, options, UDP over IPv4 without
+    a checksum, ICMP -- all verify; the same packets with a wrong L4 checksum
+    fail bit 1 only."""
+    import random
+    import struct
+
+    import numpy as np
+
+    rng = random.Random(11)
+    good, expect = [], []
+    for k in range(3000):
+        fam = rng.choice([4, 6])
+        proto = rng.choice([6, 17, 17, 1]) if fam == 4 else rng.choice([6, 17])
+        l4len = rng.randint(20 if proto == 6 else 8, 3000)
+        l4 = bytearray(rng.randbytes(l4len))
+        src, dst = rng.randbytes(4 if fam == 4 else 16), rng.randbytes(4 if fam == 4 else 16)
+        field = {6: 16, 17: 6}.get(proto)
+        if field is not None:
+            l4[field:field + 2] = b"\0\0"
+            if fam == 4 and proto == 17 and k % 7 == 0:
+                pass  # no UDP checksum over IPv4 (RFC 768): the field stays 0
+            else:
+                c = (oracle.inet_checksum(bytes(l4), proto, src, dst, l4len) if fam == 4 else
+                     oracle.inet6_checksum(bytes(l4), proto, src, dst, l4len))
+                if fam == 4 and proto == 17 and c == 0:
+                    c = 0xFFFF  # never "no checksum" by accident (either verifies: both mean zero)
+                l4[field:field + 2] = struct.pack(">H", c)
+        if fam == 4:
+            hdr = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + l4len, k & 0xFFFF, 0x4000, 64, proto, 0, src, dst))
+            c = oracle.ip_checksum(bytes(hdr))
+            hdr[10:12] = struct.pack(">H", c)
+        else:
+            hdr = bytearray(struct.pack(">IHBB16s16s", 0x60000000, l4len, proto, 64, src, dst))
+        good.append(bytes(hdr + l4) + rng.randbytes(rng.choice([0, 0, 6])))  # trailing link padding
+        expect.append(3)
+    assert (_verify(good) == 3).all()
+    broken = []
+    for p in good:
+        v4 = p[0] >> 4 == 4
+        hl = 20 if v4 else 40
+        proto = p[9] if v4 else p[6]
+        q = bytearray(p)
+        if proto == 6:
+            q[hl + 16] ^= 0x01
+        elif proto == 17 and not (v4 and q[hl + 6] == 0 and q[hl + 7] == 0):
+            q[hl + 6] ^= 0x01
+        broken.append(bytes(q))
+    ok = _verify(broken)
+    for p, o in zip(good, ok):
+        v4 = p[0] >> 4 == 4
+        proto = p[9] if v4 else p[6]
+        no_l4 = proto == 1 or (v4 and proto == 17 and p[26] == 0 and p[27] == 0)
+        assert o == (3 if no_l4 else 1), (proto, o)

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""RX batch verification rate (pip_checksum_amd_verify_packets, the drop-in's
+SURVEY 8 f2 helper) from host memory: N TCP/IPv4 packets of a given size,
+heap (copied into the queue's staging) or pinned (pipck_host_alloc: read in
+place), one call per batch.  One JSON line per (size, batch, memory).
+
+    python tools/rx_verify_bench.py [--sizes 1500,9000] [--batches 1024,16384,65536]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import statistics
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import numpy as np  # noqa: E402
+
+from pip_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1500,9000")
+    ap.add_argument("--batches", default="1024,16384,65536")
+    ap.add_argument("--reps", type=int, default=10)
+    a = ap.parse_args()
+    shim = C.CDLL(str(_lib.LIBSHIM))
+    fn = shim.pip_checksum_amd_verify_packets
+    fn.restype = C.c_uint32
+    fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p]
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    for size in (int(x) for x in a.sizes.split(",")):
+        for n in (int(x) for x in a.batches.split(",")):
+            total = size * n
+            for mem in ("heap", "pinned"):
+                if mem == "pinned":
+                    p = lib.pipck_host_alloc(total)
+                    buf = np.ctypeslib.as_array((C.c_uint8 * total).from_address(p))
+                else:
+                    buf = np.empty(total, dtype=np.uint8)
+                buf[:] = rng.integers(0, 256, total, dtype=np.uint8)
+                pk = buf.reshape(n, size)
+                pk[:, 0] = 0x45
+                pk[:, 2] = size >> 8
+                pk[:, 3] = size & 0xFF
+                pk[:, 9] = 6
+                base = buf.ctypes.data
+                ptrs = (C.c_void_p * n)(*[base + i * size for i in range(n)])
+                lens = (C.c_uint32 * n)(*([size] * n))
+                ok = np.zeros(n, dtype=np.uint8)
+                fn(ptrs, lens, n, ok.ctypes.data)  # warm
+                ts = []
+                for _ in range(a.reps):
+                    t0 = time.perf_counter()
+                    fn(ptrs, lens, n, ok.ctypes.data)
+                    ts.append(time.perf_counter() - t0)
+                t = statistics.median(ts)
+                print(json.dumps({"tool": "rx_verify_bench", "packet_bytes": size, "batch": n, "memory": mem,
+                                  "ms_per_call": round(t * 1e3, 4), "gib_per_s": round(total / t / 2**30, 3),
+                                  "mpkt_per_s": round(n / t / 1e6, 3), "verified": int((ok == 3).sum())}), flush=True)
+                del pk, buf
+                if mem == "pinned":
+                    lib.pipck_host_free(C.c_void_p(p))
+
+
+if __name__ == "__main__":
+    main()
