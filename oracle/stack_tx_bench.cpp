@@ -23,7 +23,8 @@
 //        pip's TX path with no checksum work: the ceiling of any offload (wrong wire bytes)
 //
 // --conns K opens K connections (client ports 40000+k) and writes to them in
-// turn.  --pipeline (capture modes, K >= 2) overlaps the GPU with pip: after
+// turn; --family 6 runs them over IPv6 (pip_tcp_packet.cpp:130 takes
+// pip_inet6_checksum_buf, pip_netif::output6 adds no header checksum).  --pipeline (capture modes, K >= 2) overlaps the GPU with pip: after
 // each write pip_checksum_amd_submit() starts that write's batch and completes
 // the previous one, whose packets are then output and its connection ACKed
 // while the GPU works on the next (pip waits for the ACK of a write's PUSH
@@ -162,18 +163,30 @@ void on_connect(pip_netif&, std::shared_ptr<pip_tcp> tcp, const void* hs, pip_ui
 void put16(uint8_t* p, uint16_t v) { p[0] = v >> 8; p[1] = (uint8_t)v; }
 void put32(uint8_t* p, uint32_t v) { put16(p, v >> 16); put16(p + 2, (uint16_t)v); }
 
-// a client segment to pip (10.0.0.2:port -> 10.0.0.1:80); RX takes no checksum
+unsigned g_family = 4;  // --family 6: the connections run over IPv6 (fd00::2 -> fd00::1)
+
+// a client segment to pip (10.0.0.2:port -> 10.0.0.1:80, or fd00::2 -> fd00::1);
+// RX takes no checksum
 std::vector<uint8_t> craft(uint16_t port, uint32_t seq, uint32_t ack, uint8_t flags, const std::vector<uint8_t>& opts) {
-    const size_t thl = 20 + opts.size();
-    std::vector<uint8_t> p(20 + thl, 0);
-    p[0] = 0x45;
-    put16(&p[2], (uint16_t)p.size());
-    p[8] = 64;
-    p[9] = IPPROTO_TCP;
-    const uint8_t cli[4] = {10, 0, 0, 2}, srv[4] = {10, 0, 0, 1};
-    memcpy(&p[12], cli, 4);
-    memcpy(&p[16], srv, 4);
-    uint8_t* t = &p[20];
+    const size_t thl = 20 + opts.size(), ihl = g_family == 6 ? 40 : 20;
+    std::vector<uint8_t> p(ihl + thl, 0);
+    if (g_family == 6) {
+        p[0] = 0x60;
+        put16(&p[4], (uint16_t)thl);  // payload length
+        p[6] = IPPROTO_TCP;
+        p[7] = 64;
+        p[8] = 0xfd, p[23] = 2;   // source fd00::2
+        p[24] = 0xfd, p[39] = 1;  // destination fd00::1
+    } else {
+        p[0] = 0x45;
+        put16(&p[2], (uint16_t)p.size());
+        p[8] = 64;
+        p[9] = IPPROTO_TCP;
+        const uint8_t cli[4] = {10, 0, 0, 2}, srv[4] = {10, 0, 0, 1};
+        memcpy(&p[12], cli, 4);
+        memcpy(&p[16], srv, 4);
+    }
+    uint8_t* t = &p[ihl];
     put16(t, port);
     put16(t + 2, 80);
     put32(t + 4, seq);
@@ -208,6 +221,7 @@ int main(int argc, char** argv) {
         else if (a == "--conns") conns = (unsigned)atoi(val());
         else if (a == "--pipeline") pipeline = true;
         else if (a == "--dump") g_dump = fopen(val(), "wb");
+        else if (a == "--family") g_family = (unsigned)atoi(val());
         else { fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }
     if (mode == "ref") g_mode = REF;
@@ -223,8 +237,9 @@ int main(int argc, char** argv) {
 #else
     if (g_mode == REF) { fprintf(stderr, "this build links libpip_checksum_amd.so: sync/capture/capture_zc\n"); return 2; }
 #endif
-    if (mss < 1 || mss > 65495 || per_write < 1 || per_write > (1u << 30) || conns < 1 || conns > 64) {
-        fprintf(stderr, "bad --mss / --write / --conns\n");
+    if (mss < 1 || mss > 65495 || per_write < 1 || per_write > (1u << 30) || conns < 1 || conns > 64 ||
+        (g_family != 4 && g_family != 6)) {
+        fprintf(stderr, "bad --mss / --write / --conns / --family\n");
         return 2;
     }
     if (pipeline && (conns < 2 || (g_mode != CAPTURE && g_mode != CAPTURE_ZC))) {
@@ -258,11 +273,17 @@ int main(int argc, char** argv) {
     uint8_t z[20] = {0};
     struct in_addr a4;
     a4.s_addr = 0x0100000a;
+    struct in6_addr a6;
+    memset(&a6, 0, sizeof a6);
     auto warm = [&]() {
         auto head = std::make_shared<pip_buf>(20);
         head->set_next(std::make_shared<pip_buf>(buf, (pip_uint32)(per_write < 1460 ? per_write : 1460), 0));
-        (void)pip_ip_checksum(z, 20);
-        (void)pip_inet_checksum_buf(head, IPPROTO_TCP, a4, a4);
+        if (g_family == 6) {
+            (void)pip_inet6_checksum_buf(head, IPPROTO_TCP, a6, a6);
+        } else {
+            (void)pip_ip_checksum(z, 20);
+            (void)pip_inet_checksum_buf(head, IPPROTO_TCP, a4, a4);
+        }
     };
     double cold[3] = {0, 0, 0};  // seconds: first synchronous calls, first and second capture flush
     double tw = now();
@@ -355,11 +376,11 @@ int main(int argc, char** argv) {
         pip_checksum_amd_capture(false);
     }
 #endif
-    printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
+    printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"family\": %u, \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
            "\"writes\": %u, \"conns\": %u, \"pipeline\": %s, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
            "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu, "
            "\"cold_ms\": {\"first_calls\": %.3f, \"first_flush\": %.3f, \"second_flush\": %.3f}}\n",
-           mode.c_str(), mss, per_write, sent, writes, conns, pipeline ? "true" : "false", (unsigned long long)pk, el, sent / el / (1u << 30),
+           mode.c_str(), g_family, mss, per_write, sent, writes, conns, pipeline ? "true" : "false", (unsigned long long)pk, el, sent / el / (1u << 30),
            pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
            (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load(), cold[0] * 1e3, cold[1] * 1e3,
            cold[2] * 1e3);

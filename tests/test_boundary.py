@@ -60,9 +60,9 @@ def test_pip_stack_on_amd_checksum_is_byte_identical(capture):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mss", [1460, 8960])
-def test_pip_tx_path_at_volume_matches_pip(mss):
-    """pip's TCP write() path at volume (oracle/stack_tx_bench.cpp): pip's own
+@pytest.mark.parametrize("family,mss", [(4, 1460), (4, 8960), (6, 1440)])
+def test_pip_tx_path_at_volume_matches_pip(family, mss):
+    """pip's TCP write() path at volume over IPv4 and IPv6 (oracle/stack_tx_bench.cpp): pip's own
     build vs the drop-in synchronously, in capture mode, with zero-copy, and
     pipelined across two connections -- FNV-1a over every emitted wire byte must
     be identical, and pip's retransmit timer must never fire."""
@@ -74,7 +74,8 @@ def test_pip_tx_path_at_volume_matches_pip(mss):
     assert ref_bin.exists() and amd_bin.exists(), "build with `make -C oracle ref ref-amd`"
 
     def run(binary, *args):
-        cmd = [str(binary), "--mss", str(mss), "--bytes", str(8 << 20), "--write", str(1 << 20), "--verify", *args]
+        cmd = [str(binary), "--family", str(family), "--mss", str(mss), "--bytes", str(8 << 20), "--write", str(1 << 20),
+               "--verify", *args]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=dict(os.environ))
         if r.returncode == 3 and "retransmit:" in r.stderr:
             # exit 3 = pip's 1 s timer resent a segment (a host-side stall, e.g. during the
