@@ -29,6 +29,7 @@ namespace {
 struct ThreadCtx {
     pipck_ctx* ctx = nullptr;
     pipck_txq* txq = nullptr;
+    pipck_txq* rxq = nullptr;  // pip_checksum_amd_verify_packets: received packets, never pip's TX batch
     bool zero_copy = false;  // pip_checksum_amd_zero_copy(): pinned segments read in place at flush
     bool capture = false;    // pip_checksum_amd_capture(): pip's TX calls queue instead of computing
     // Chains whose pinned segments a batch reads in place stay referenced until
@@ -36,6 +37,7 @@ struct ThreadCtx {
     // `keep` for the batch receiving adds, `keep_inflight` for the submitted one.
     std::vector<std::shared_ptr<pip_buf>> keep, keep_inflight;
     ~ThreadCtx() {
+        if (rxq) pipck_txq_destroy(rxq);
         if (txq) pipck_txq_destroy(txq);  // waits for the in-flight batch
         keep.clear();
         keep_inflight.clear();
@@ -254,23 +256,17 @@ void pip_checksum_amd_capture(bool on) { t_ctx.capture = on; }
 // that verifies, and the queue stores that result into a scratch word.
 namespace {
 
-struct RxCtx {
-    pipck_txq* q = nullptr;
-    ~RxCtx() {
-        if (q) pipck_txq_destroy(q);
-    }
-};
-thread_local RxCtx t_rx;  // first used after t_ctx, so destroyed before it
-
+// this thread's RX queue (a member of the thread's context, so it is destroyed
+// before the HIP context it was created on)
 pipck_txq* rx_queue() {
-    if (!t_rx.q) {
-        int rc = pipck_txq_create(t_ctx.get(), &t_rx.q);
+    if (!t_ctx.rxq) {
+        int rc = pipck_txq_create(t_ctx.get(), &t_ctx.rxq);
         if (rc) die("pipck_txq_create", rc);
         // packets already in pinned memory (a registered tun read ring) are read in place
-        rc = pipck_txq_auto_zero_copy(t_rx.q, 1);
+        rc = pipck_txq_auto_zero_copy(t_ctx.rxq, 1);
         if (rc) die("pipck_txq_auto_zero_copy", rc);
     }
-    return t_rx.q;
+    return t_ctx.rxq;
 }
 
 uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }

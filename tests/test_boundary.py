@@ -178,6 +178,15 @@ def test_rx_verify_accepts_what_pip_emits_and_rejects_corruption():
         assert o == 3 - w, (o, w)  # exactly the damaged checksum fails
     junk = [b"", bytes(10), bytes([0x45]) + bytes(10), bytes([0x45, 0, 0xFF, 0xFF]) + bytes(16), bytes([0x60]) + bytes(20)]
     assert (_verify(junk) == 0).all()
+    # a thread whose FIRST drop-in call is the verifier, then exits: its RX queue is
+    # torn down before its HIP context (thread_local destruction order)
+    import threading
+
+    res = {}
+    t = threading.Thread(target=lambda: res.setdefault("ok", _verify(pkts)))
+    t.start()
+    t.join()
+    assert (res["ok"] == 3).all()
 
 
 @pytest.mark.gpu
