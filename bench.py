@@ -14,10 +14,13 @@ synthetic packets already resident in HBM (generated on the device from
 global packet ids; cfg5 = 8,980-byte TCP/IPv4 segments, 8M packets per GPU,
 64M at 8 GPUs -> weak scaling).  Ranks share nothing on the data path: fixed
 configs split the global packet-id range evenly, ragged ones (cfg4) at equal
-L4 bytes.  gloo carries the barrier, the MAX of elapsed times and the per-rank
-figures.  Rank 0 prints ONE JSON line.
+L4 bytes.  gloo carries the barrier, every rank's start and end on the
+node's shared monotonic clock and the per-rank figures.  Rank 0 prints ONE
+JSON line.
 
-value   = checksummed L4 bytes of all ranks x K / max-over-ranks wall time, GiB/s
+value   = checksummed L4 bytes of all ranks x K / (latest end - earliest start)
+          over ranks, GiB/s; the max-over-ranks elapsed time and
+          the start skew after the barrier are reported beside it
 roofline: algorithmic bytes per launch (L + 2 per packet: L read, u16 written)
           / the MEDIAN per-dispatch duration (a HIP event pair around every
           launch, on the launch stream), vs 8 TB/s; the back-to-back mean is
@@ -68,6 +71,8 @@ def parse(argv=None):
     p.add_argument("--traffic", default="auto",
                    help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json); "
                         "attached only if measured on this exact kernel of this exact libpipck.so build")
+    p.add_argument("--start-skew-ms", type=float, default=0.0,
+                   help="rehearsal/test only: rank r waits r x this after the barrier before its timed start")
     p.add_argument("--share-gpus", action="store_true",
                    help="allow more ranks than visible GPUs (ranks then share devices; rehearsal only)")
     return p.parse_args(argv)
@@ -146,14 +151,16 @@ def run_rank(args) -> int:
     # rehearsal), and never silently: the line then says the GPUs were shared
     n_dev = torch.cuda.device_count()
     try:
-        dev = shard.device_for_rank(env.local_rank, env.world, n_dev, args.share_gpus)
+        dev = shard.device_for_rank(env.local_rank, shard.local_world_size(env), n_dev, args.share_gpus)
     except ValueError as e:
         print(f"bench.py: {e}", file=sys.stderr)
         shard.shutdown(env)
         return 3
     torch.cuda.set_device(dev)
     engine.require_gpu()
-    placement = {"rank": env.rank, "device": dev, "pci_bus_id": engine.pci_bus_id(dev),
+    import socket
+
+    placement = {"rank": env.rank, "host": socket.gethostname(), "device": dev, "pci_bus_id": engine.pci_bus_id(dev),
                  "name": torch.cuda.get_device_name(dev)}
     w = workload(args.workload)
     per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
@@ -196,31 +203,35 @@ def run_rank(args) -> int:
 
     for _ in range(args.warmup):
         step(out)
-    torch.cuda.synchronize()
-    shard.barrier(env)
 
     # an event pair around every launch, on the launch stream (engine launches on
     # torch's current stream): per-dispatch durations without a profiler
     ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
+
+    def timed_step(i):
         ev_s[i].record()
         step(out)
         ev_e[i].record()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    shard.barrier(env)
+
+    skew = (lambda: time.sleep(env.rank * args.start_skew_ms / 1e3)) if args.start_skew_ms else None
+    t0, t1 = shard.timed_steps(env, args.steps, timed_step, torch.cuda.synchronize, before_start=skew)
     kernel = last_kernel()  # the instantiation the timed launches ran
-    elapsed = shard.max_over_ranks(env, t1 - t0)
     per_launch = sorted(s.elapsed_time(e) / 1e3 for s, e in zip(ev_s, ev_e))
     launch_s = per_launch[len(per_launch) // 2] if args.steps % 2 else \
         (per_launch[args.steps // 2 - 1] + per_launch[args.steps // 2]) / 2
     b2b_s = ev_s[0].elapsed_time(ev_e[-1]) / 1e3 / args.steps
-    ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), t1 - t0, launch_s])
+    ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), (t1 - t0) / 1e9, launch_s])
+    clocks = shard.gather_ints(env, [t0, t1])
     placements = shard.gather_objects(env, placement)
     total_bytes = sum(r[0] for r in ranks)
     total_pkts = sum(r[1] for r in ranks)
+    one_host = len({p["host"] for p in placements}) == 1
+    agg = shard.aggregate([c[0] for c in clocks], [c[1] for c in clocks], [r[0] for r in ranks], args.steps)
+    # ranks on one node share CLOCK_MONOTONIC: the span from the earliest start to
+    # the latest end; across nodes the clocks differ and only each
+    # rank's own elapsed time is comparable
+    elapsed = agg["span_s"] if one_host else agg["max_rank_s"]
 
     gib_s = total_bytes * args.steps / elapsed / 2**30
     # L4 payload only: the checksummed bytes minus the TCP (20 B) /
@@ -240,7 +251,7 @@ def run_rank(args) -> int:
         if traffic is not None and t.get("rocprof_timed_median_ns"):
             rocprof_ms = t["rocprof_timed_median_ns"] / 1e6
     launch_bound = launch_s < LAUNCH_BOUND_S
-    n_shared = env.world - len({p["pci_bus_id"] for p in placements})
+    n_shared = env.world - len({(p["host"], p["pci_bus_id"]) for p in placements})
 
     line = {
         "metric": METRIC,
@@ -272,6 +283,16 @@ def run_rank(args) -> int:
         # each rank's own rate over its own wall time and shard
         "per_rank_gib_per_s": [round(r[0] * args.steps / r[2] / 2**30, 2) for r in ranks],
         "per_rank_packets": [int(r[1]) for r in ranks],
+        "timing": {
+            "value_over": "latest end - earliest start over ranks (one node's monotonic clock)" if one_host
+                          else "max over ranks of each rank's own elapsed time (ranks on several hosts)",
+            "span_ms": round(agg["span_s"] * 1e3, 4),
+            "max_rank_elapsed_ms": round(agg["max_rank_s"] * 1e3, 4),
+            "start_skew_ms": round(agg["start_skew_ms"], 4),
+            "end_skew_ms": round(agg["end_skew_ms"], 4),
+            "value_by_max_rank_elapsed": round(agg["rate_max_rank"] / 2**30, 2),
+            "injected_start_skew_ms_per_rank": args.start_skew_ms or None,
+        },
         "devices_visible": n_dev,
         "distinct_gpus": env.world - n_shared,
         "per_rank_device": placements,

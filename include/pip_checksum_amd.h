@@ -97,14 +97,31 @@ bool pip_checksum_amd_capturing();
 
 // ---- RX batch verification (pip itself never verifies) ----
 // Verify n received IP packets (as read from the tun device: IPv4 or IPv6,
-// pkts[i] of lens[i] bytes) in one GPU batch on this thread.  ok[i] bit 0 =
-// the IPv4 header checksum verifies (always set for IPv6), bit 1 = the TCP or
-// UDP checksum over its pseudo-header verifies (also set when the packet
-// carries none this verifies: another protocol, or UDP over IPv4 with a zero
-// checksum, RFC 768); ok[i] == 3 = accept.  A malformed packet (lengths that do
-// not fit, not IPv4/IPv6) gets 0.  Packets in pinned memory are read in place;
-// the call returns when every result is known.  Returns the number of packets
-// with ok == 3.  Uses its own queue: pip's deferred TX batch is not touched.
+// pkts[i] of lens[i] bytes) in one GPU batch on this thread.  ok[i] bits:
+//   PIP_RX_IP_OK       the IPv4 header checksum verifies (always set for IPv6)
+//   PIP_RX_L4_OK       no payload checksum failed: it verified, or there was
+//                      none this call can check (see PIP_RX_L4_CHECKED)
+//   PIP_RX_L4_CHECKED  the payload's checksum WAS computed: TCP or UDP over its
+//                      pseudo-header, ICMPv4 over the message alone (RFC 792;
+//                      pip_ip_checksum's arithmetic), ICMPv6 over the IPv6
+//                      pseudo-header with next header 58 (RFC 4443 2.3)
+// ok[i] == PIP_RX_VERIFIED (7): both checksums computed and verified.
+// ok[i] == PIP_RX_IP_OK | PIP_RX_L4_OK (3): nothing failed but the payload was
+// NOT checked -- an IPv4 fragment (MF or offset set: its L4 checksum spans the
+// reassembled datagram), UDP over IPv4 with a zero checksum (RFC 768), an IPv6
+// fragment or routing header, another protocol.  A caller that must not pass
+// unchecked packets accepts 7 only.  A damaged checksum clears its OK bit (a
+// checked-and-failed payload reads PIP_RX_L4_CHECKED without PIP_RX_L4_OK); a
+// malformed packet (lengths that do not fit, a truncated TCP/UDP/ICMP header,
+// not IPv4/IPv6) gets no L4 bits, or 0.  IPv6 hop-by-hop / destination-options
+// headers and atomic fragments are walked to the upper layer.  Packets in
+// pinned memory are read in place; the call returns when every result is
+// known.  Returns the number of packets with ok == PIP_RX_VERIFIED.  Uses its
+// own queue: pip's deferred TX batch is not touched.
+#define PIP_RX_IP_OK 1u
+#define PIP_RX_L4_OK 2u
+#define PIP_RX_L4_CHECKED 4u
+#define PIP_RX_VERIFIED 7u
 extern "C" uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n,
                                                     uint8_t* ok);
 

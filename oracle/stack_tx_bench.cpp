@@ -38,11 +38,12 @@
 #include "pip_checksum.h"
 #include "protocol/pip_tcp.h"
 
-#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unistd.h>
@@ -66,6 +67,9 @@ struct Conn {
     uint32_t cseq = 7000;
     uint32_t srv_next = 0;  // pip's next sequence number on this connection, from its emitted segments
     uint8_t* buf = nullptr;
+    // segments pip sent and the peer has not ACKed yet (the ones pip's timer may
+    // resend): sequence number and the time pip sent it, oldest first (g_sent_mu)
+    std::deque<std::pair<uint32_t, double>> unacked;
 };
 std::vector<Conn> g_conns;
 int g_connecting = -1;  // the connection whose SYN is being input
@@ -120,22 +124,56 @@ void emit(const std::vector<std::shared_ptr<pip_buf>>& segs) {
 }
 
 std::thread::id g_main;
-std::atomic<uint64_t> g_retransmits{0};
+std::mutex g_sent_mu;                     // Conn::unacked: the main thread sends, pip's timer thread resends
+uint64_t g_resends_stalled = 0;           // resent at >= 1 s of age: a real stall (the run fails)
+uint64_t g_resends_stale_clock = 0;       // resent younger than 1 s: pip's timer race (below)
+double g_max_resend_age = 0, g_max_unacked = 0;
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
 
 void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
-    // pip's timer thread resends a segment left unacknowledged for 1 s
-    // (pip/protocol/pip_tcp_check.cpp:25-39); it never should here, and a run where
-    // it did is reported as invalid rather than digested
+    auto q = buf->next();  // the TCP header segment
+    const uint8_t* th = q && q->payload_len() >= 14 ? (const uint8_t*)q->payload() : nullptr;
+    const unsigned k = th ? (unsigned)(th[2] << 8 | th[3]) - kPortBase : ~0u;  // pip's destination = the client port
     if (std::this_thread::get_id() != g_main) {
-        g_retransmits++;
-        auto q = buf->next();  // the TCP header segment: which packet pip resent
-        if (q && q->payload_len() >= 14) {
-            const uint8_t* th = (const uint8_t*)q->payload();
-            fprintf(stderr, "retransmit: port %u seq %u flags 0x%02x at %.3f s\n", (unsigned)(th[2] << 8 | th[3]),
-                    (uint32_t)th[4] << 24 | (uint32_t)th[5] << 16 | (uint32_t)th[6] << 8 | th[7], th[13],
-                    std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count());
+        // pip's timer thread resends the oldest unacknowledged segment once it is
+        // 1 s old (pip/protocol/pip_tcp_check.cpp:25-39).  Its age here tells a
+        // stall (>= 1 s: the run fails) from pip's own timer race: timer_tick
+        // reads the clock BEFORE it takes the connection's mutex
+        // (pip_tcp_check.cpp:45-56), so a segment sent while the timer waited on
+        // that mutex is newer than the timer's `now`, and the unsigned
+        // `now - send_time` (:30) wraps to a huge age.  pip's own build does
+        // this too (profiles/r04_pip_timer_race.jsonl).  Either way the resent
+        // copy is not digested: the wire digest covers the main thread's packets.
+        double age = -1;
+        const uint32_t seq = th ? rd32(th + 4) : 0;
+        {
+            std::lock_guard<std::mutex> g(g_sent_mu);
+            if (k < g_conns.size())
+                for (auto& u : g_conns[k].unacked)
+                    if (u.first == seq) { age = now() - u.second; break; }
+            if (age >= 0 && age < 1.0) g_resends_stale_clock++;
+            else g_resends_stalled++;
+            if (age > g_max_resend_age) g_max_resend_age = age;
         }
+        if (th)
+            fprintf(stderr, "resend by pip's timer: port %u seq %u flags 0x%02x at %.3f s, %s\n",
+                    (unsigned)(th[2] << 8 | th[3]), seq, th[13], now(),
+                    age < 0 ? "not an unacknowledged segment" :
+                    age < 1.0 ? "younger than 1 s (pip's stale-clock race)" : "unacknowledged for >= 1 s (a stall)");
         return;
+    }
+    if (th && k < g_conns.size()) {
+        size_t data = 0;
+        for (auto p = q->next(); p; p = p->next()) data += p->payload_len();
+        if (data || (th[13] & (TH_SYN | TH_FIN))) {  // queued for retransmission by pip
+            std::lock_guard<std::mutex> g(g_sent_mu);
+            g_conns[k].unacked.emplace_back(rd32(th + 4), now());
+        }
     }
     std::vector<std::shared_ptr<pip_buf>> segs;
     for (auto q = buf; q; q = q->next()) segs.push_back(q);
@@ -144,6 +182,27 @@ void on_output(pip_netif&, std::shared_ptr<pip_buf> buf) {
     else
         emit(segs);
 }
+
+// the peer's ACK of everything sent on connection k has been input: nothing is
+// left for pip's timer; the oldest segment's age is the longest any waited
+void acked(unsigned k) {
+    std::lock_guard<std::mutex> g(g_sent_mu);
+    auto& u = g_conns[k].unacked;
+    if (!u.empty() && now() - u.front().second > g_max_unacked) g_max_unacked = now() - u.front().second;
+    u.clear();
+}
+
+// the longest single stack action of the run (an input, a write, a flush)
+struct ActionClock {
+    double max = 0;
+    const char* which = "none";
+    double t = 0;
+    void start() { t = now(); }
+    void stop(const char* what) {
+        const double d = now() - t;
+        if (d > max) max = d, which = what;
+    }
+} g_act;
 
 // after each stack action: capture modes store every queued field, then output the packets
 void settle() {
@@ -196,10 +255,6 @@ std::vector<uint8_t> craft(uint16_t port, uint32_t seq, uint32_t ack, uint8_t fl
     put16(t + 14, 65535);  // << 14 (the SYN's window-scale option): a 1 GiB send window
     memcpy(t + 20, opts.data(), opts.size());
     return p;
-}
-
-double now() {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 }  // namespace
@@ -311,22 +366,31 @@ int main(int argc, char** argv) {
         Conn& c = g_conns[k];
         g_connecting = (int)k;
         auto syn = craft(c.port, c.cseq, 0, TH_SYN, opts);
-        const double ts = now();
+        g_act.start();
         nif.input(syn.data());
         settle();
-        // the SYN-ACK stays unacknowledged until the ACK below: a stall here past
-        // pip's 1 s timer makes it resend (reported, and the run fails)
-        if (now() - ts > 0.1) fprintf(stderr, "slow handshake: SYN -> SYN-ACK out took %.3f s\n", now() - ts);
+        g_act.stop("syn -> syn-ack");
         if (!c.tcp) { fprintf(stderr, "no connection %u\n", k); return 1; }
         c.cseq += 1;
         auto ack = craft(c.port, c.cseq, c.srv_next, TH_ACK, {});
+        g_act.start();
         nif.input(ack.data());
+        acked(k);
         settle();
+        g_act.stop("handshake ack");
     }
     g_connecting = -1;
     auto ack_conn = [&](unsigned k) {  // the peer ACKs everything pip sent on connection k (and its PUSH)
         auto a = craft(g_conns[k].port, g_conns[k].cseq, g_conns[k].srv_next, TH_ACK, {});
+        g_act.start();
         nif.input(a.data());
+        acked(k);
+        g_act.stop("ack input");
+    };
+    auto settle_timed = [&]() {
+        g_act.start();
+        settle();
+        g_act.stop("flush");
     };
 
     const uint64_t pk0 = g_packets;
@@ -339,14 +403,18 @@ int main(int argc, char** argv) {
     while (sent < total) {
         const unsigned k = writes % conns;
         const size_t want = total - sent < per_write ? total - sent : per_write;
+        g_act.start();
         const uint32_t w = g_conns[k].tcp->write(g_conns[k].buf, (pip_uint32)want, false);
+        g_act.stop("write");
         if (w == 0) { fprintf(stderr, "write stalled at %zu bytes\n", sent); return 1; }
         sent += w;
         writes++;
 #ifdef PIPCK_AMD
         if (pipeline) {
             // start this write's batch; the previous one completes (fields stored)
+            g_act.start();
             pip_checksum_amd_submit();
+            g_act.stop("submit");
             for (auto& sg : inflight) emit(sg);
             inflight.clear();
             if (prev >= 0) ack_conn((unsigned)prev);
@@ -355,17 +423,19 @@ int main(int argc, char** argv) {
             continue;
         }
 #endif
-        settle();
+        settle_timed();
         ack_conn(k);
-        settle();
+        settle_timed();
     }
 #ifdef PIPCK_AMD
     if (pipeline) {
+        g_act.start();
         pip_checksum_amd_complete();
+        g_act.stop("complete");
         for (auto& sg : inflight) emit(sg);
         inflight.clear();
         if (prev >= 0) ack_conn((unsigned)prev);
-        settle();
+        settle_timed();
     }
 #endif
     const double el = now() - t0;
@@ -376,15 +446,30 @@ int main(int argc, char** argv) {
         pip_checksum_amd_capture(false);
     }
 #endif
+    uint64_t stalled, stale;
+    double max_age, max_unacked;
+    {
+        std::lock_guard<std::mutex> g(g_sent_mu);
+        stalled = g_resends_stalled, stale = g_resends_stale_clock;
+        max_age = g_max_resend_age, max_unacked = g_max_unacked;
+    }
+    // retransmits: segments pip resent after waiting >= 1 s for their ACK (or not
+    // found unacknowledged) -- a stall, and the run fails with exit 3;
+    // stale_clock_resends: pip's timer race, younger segments (on_output above);
+    // max_action_ms: the longest single input / write / flush of the run;
+    // max_unacked_ms: the longest any segment waited for the peer's ACK (pip's
+    // timer resends at 1,000)
     printf("{\"tool\": \"stack_tx_bench\", \"mode\": \"%s\", \"family\": %u, \"mss\": %u, \"write_bytes\": %zu, \"payload_bytes\": %zu, "
            "\"writes\": %u, \"conns\": %u, \"pipeline\": %s, \"packets\": %llu, \"seconds\": %.6f, \"payload_gib_per_s\": %.4f, \"mpkt_per_s\": %.4f, "
            "\"digest\": \"%016llx\", \"digest_of\": \"%s\", \"wire_bytes\": %llu, \"retransmits\": %llu, "
+           "\"stale_clock_resends\": %llu, \"max_resend_age_ms\": %.3f, \"max_action_ms\": %.3f, \"max_action\": \"%s\", "
+           "\"max_unacked_ms\": %.3f, "
            "\"cold_ms\": {\"first_calls\": %.3f, \"first_flush\": %.3f, \"second_flush\": %.3f}}\n",
            mode.c_str(), g_family, mss, per_write, sent, writes, conns, pipeline ? "true" : "false", (unsigned long long)pk, el, sent / el / (1u << 30),
            pk / el / 1e6, (unsigned long long)g_digest, g_verify ? "every wire byte" : "ip_sum, th_sum, length",
-           (unsigned long long)g_wire_bytes, (unsigned long long)g_retransmits.load(), cold[0] * 1e3, cold[1] * 1e3,
-           cold[2] * 1e3);
+           (unsigned long long)g_wire_bytes, (unsigned long long)stalled, (unsigned long long)stale, max_age * 1e3,
+           g_act.max * 1e3, g_act.which, max_unacked * 1e3, cold[0] * 1e3, cold[1] * 1e3, cold[2] * 1e3);
     fflush(stdout);
     if (g_dump) fclose(g_dump);
-    _exit(g_retransmits.load() ? 3 : 0);  // pip's timer thread is detached and never stops
+    _exit(stalled ? 3 : 0);  // pip's timer thread is detached and never stops
 }

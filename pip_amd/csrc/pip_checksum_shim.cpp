@@ -271,13 +271,41 @@ pipck_txq* rx_queue() {
 
 uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
 
+// The upper-layer header of an IPv6 packet: walks the extension headers whose
+// presence does not change the pseudo-header (hop-by-hop 0, destination
+// options 60, an atomic fragment 44).  Returns false when the payload's
+// checksum cannot be checked from this packet alone -- a real fragment (offset
+// or M flag set), a routing header 43 (the pseudo-header takes the FINAL
+// destination), or a chain too long or running past the payload.
+bool ipv6_upper(const uint8_t* b, uint32_t plen, uint8_t* proto, uint32_t* off) {
+    uint8_t nh = b[6];
+    uint32_t at = 40;
+    for (int k = 0; k < 8; k++) {
+        if (nh != 0 && nh != 60 && nh != 44) {
+            *proto = nh;
+            *off = at;
+            return nh != 43;
+        }
+        if (at + 8 > 40 + plen) return false;
+        const uint8_t* e = b + at;
+        if (nh == 44) {
+            if (rd16(e + 2) & 0xFFF9u) return false;  // fragment offset (bits 15-3) or M (bit 0) set
+            at += 8;
+        } else {
+            at += 8u * (e[1] + 1u);
+        }
+        nh = e[0];
+    }
+    return false;
+}
+
 }  // namespace
 
 uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n, uint8_t* ok) {
     if (!n) return 0;
     if (!pkts || !lens || !ok) die("pip_checksum_amd_verify_packets: null argument", PIPCK_EINVAL);
     std::vector<uint16_t> ip_res(n, 0xFFFFu), l4_res(n, 0xFFFFu);  // htons(result) lands here; 0 = verified
-    std::vector<uint8_t> queued(n, 0);                              // bit 0: IP header queued, bit 1: segment
+    std::vector<uint8_t> queued(n, 0);                              // bit 0: IP header queued, bit 1: L4 message
     pipck_txq* q = rx_queue();
     for (uint32_t i = 0; i < n; i++) {
         ok[i] = 0;
@@ -288,46 +316,64 @@ uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t
         uint32_t l4len = 0;
         uint8_t proto = 0;
         int rc = 0;
-        if ((b[0] >> 4) == 4) {
+        const bool v4 = (b[0] >> 4) == 4;
+        if (v4) {
             const uint32_t ihl = (b[0] & 15u) * 4u, total = rd16(b + 2);
             if (ihl < 20 || total < ihl || total > len) continue;  // malformed: 0
             rc = pipck_txq_add_ip(q, b, ihl, &ip_res[i]);          // the header with its ip_sum
             if (rc) die("pipck_txq_add_ip", rc);
             queued[i] |= 1;
+            if (rd16(b + 6) & 0x3FFFu) {  // MF or a fragment offset: the L4 checksum spans the reassembled datagram
+                ok[i] |= PIP_RX_L4_OK;
+                continue;
+            }
             proto = b[9], l4 = b + ihl, l4len = total - ihl;
         } else if ((b[0] >> 4) == 6 && len >= 40) {
             const uint32_t plen = rd16(b + 4);
             if (40 + plen > len) continue;
-            ok[i] |= 1;  // IPv6 has no header checksum
-            proto = b[6], l4 = b + 40, l4len = plen;  // TCP / UDP directly after the fixed header
+            ok[i] |= PIP_RX_IP_OK;  // IPv6 has no header checksum
+            uint32_t off = 40;
+            if (!ipv6_upper(b, plen, &proto, &off)) {
+                ok[i] |= PIP_RX_L4_OK;  // not checkable from this packet (fragment, routing header)
+                continue;
+            }
+            l4 = b + off, l4len = 40 + plen - off;
         } else {
             continue;
         }
-        if ((proto != IPPROTO_TCP && proto != IPPROTO_UDP)) {
-            ok[i] |= 2;  // no checksum this helper verifies (ICMP, extension headers, ...)
+        const bool icmp = v4 ? proto == IPPROTO_ICMP : proto == IPPROTO_ICMPV6;
+        if (proto != IPPROTO_TCP && proto != IPPROTO_UDP && !icmp) {
+            ok[i] |= PIP_RX_L4_OK;  // a protocol without a checksum this helper knows: unchecked
             continue;
         }
-        if (l4len < (proto == IPPROTO_TCP ? 20u : 8u)) continue;    // truncated segment: bit 1 stays clear
-        if (proto == IPPROTO_UDP && (b[0] >> 4) == 4 && !l4[6] && !l4[7]) {
-            ok[i] |= 2;  // UDP over IPv4 without a checksum (RFC 768)
+        if (l4len < (proto == IPPROTO_TCP ? 20u : 8u)) continue;  // truncated: L4 bits stay clear
+        if (proto == IPPROTO_UDP && v4 && !l4[6] && !l4[7]) {
+            ok[i] |= PIP_RX_L4_OK;  // UDP over IPv4 without a checksum (RFC 768): unchecked
             continue;
         }
         const pipck_hseg seg{l4, l4len};
-        uint32_t src = 0, dst = 0;  // network order, as in struct in_addr
-        std::memcpy(&src, b + 12, 4);
-        std::memcpy(&dst, b + 16, 4);
-        rc = (b[0] >> 4) == 4 ? pipck_txq_add4(q, &seg, 1, proto, src, dst, &l4_res[i])
-                              : pipck_txq_add6(q, &seg, 1, proto, b + 8, b + 24, &l4_res[i]);
-        if (rc) die("pipck_txq_add", rc);
+        if (icmp && v4) {
+            // ICMPv4: pip_ip_checksum over the whole message, no pseudo-header (RFC 792)
+            rc = pipck_txq_add_ip(q, l4, l4len, &l4_res[i]);
+        } else if (v4) {
+            uint32_t src = 0, dst = 0;  // network order, as in struct in_addr
+            std::memcpy(&src, b + 12, 4);
+            std::memcpy(&dst, b + 16, 4);
+            rc = pipck_txq_add4(q, &seg, 1, proto, src, dst, &l4_res[i]);
+        } else {
+            // TCP, UDP and ICMPv6 (next header 58, RFC 4443 2.3) over the IPv6 pseudo-header
+            rc = pipck_txq_add6(q, &seg, 1, proto, b + 8, b + 24, &l4_res[i]);
+        }
+        if (rc) die("pipck_txq_add (rx)", rc);
         queued[i] |= 2;
     }
     int rc = pipck_txq_flush(q);
     if (rc) die("pipck_txq_flush", rc);
     uint32_t good = 0;
     for (uint32_t i = 0; i < n; i++) {
-        if ((queued[i] & 1) && ip_res[i] == 0) ok[i] |= 1;
-        if ((queued[i] & 2) && l4_res[i] == 0) ok[i] |= 2;
-        good += ok[i] == 3;
+        if ((queued[i] & 1) && ip_res[i] == 0) ok[i] |= PIP_RX_IP_OK;
+        if (queued[i] & 2) ok[i] |= (l4_res[i] == 0 ? PIP_RX_L4_OK : 0) | PIP_RX_L4_CHECKED;
+        good += ok[i] == PIP_RX_VERIFIED;
     }
     return good;
 }

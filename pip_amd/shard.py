@@ -5,12 +5,14 @@ packet-id ranges, one per rank (one process per GPU).  There is no exchange
 step and therefore no collective on the data path: each rank generates its
 own shard on its own device from global packet ids and checksums it in
 place.  The only cross-rank traffic is control: a barrier around the timed
-region and a MAX of the per-rank elapsed times, over gloo (CPU), so RCCL is
-never initialised.
+region and every rank's start and end on the node's shared monotonic clock,
+over gloo (CPU), so RCCL is never initialised.  The aggregate rate is
+SURVEY.md 8e's: all ranks' units / (latest end - earliest start).
 """
 from __future__ import annotations
 
 import os
+import time
 from bisect import bisect_left
 from dataclasses import dataclass
 
@@ -121,17 +123,57 @@ def byte_cuts(prefix_bytes, world: int) -> list[int]:
     return cuts
 
 
-def device_for_rank(local_rank: int, world: int, n_devices: int, share: bool = False) -> int:
-    """One GPU per rank: rank r takes device r.  More ranks than visible GPUs is
-    refused unless ``share`` (a rehearsal of N>1 on fewer GPUs, which the bench
-    line then reports as shared) -- so an N-GPU line can never silently claim
-    GPUs it did not run on."""
+def device_for_rank(local_rank: int, local_world: int, n_devices: int, share: bool = False) -> int:
+    """One GPU per rank: local rank r takes device r of its node.  More ranks on
+    a node (``local_world``, torchrun's LOCAL_WORLD_SIZE) than GPUs visible there
+    is refused unless ``share`` (a rehearsal of N>1 on fewer GPUs, which the
+    bench line then reports as shared) -- so an N-GPU line can never silently
+    claim GPUs it did not run on."""
     if n_devices < 1:
         raise ValueError("no visible GPU")
-    if world > n_devices and not share:
-        raise ValueError(f"{world} ranks but only {n_devices} visible GPU(s); pass --share-gpus to let ranks "
-                         "share devices (the line then says so)")
+    if local_world > n_devices and not share:
+        raise ValueError(f"{local_world} ranks on this node but only {n_devices} visible GPU(s); pass --share-gpus "
+                         "to let ranks share devices (the line then says so)")
     return local_rank % n_devices
+
+
+def local_world_size(env: "DistEnv") -> int:
+    """Ranks on this node: LOCAL_WORLD_SIZE (torch.distributed.run and
+    spawn_ranks set it), else the whole world (a one-node job)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", env.world))
+
+
+def timed_steps(env: "DistEnv", steps: int, step, sync, before_start=None) -> tuple[int, int]:
+    """The timed region of one rank: sync + barrier, then ``step(i)`` for i < steps,
+    then sync, bracketed by this rank's start and end on CLOCK_MONOTONIC (ns),
+    which every process of the node shares, so ranks' times compare directly.
+    ``before_start`` runs between the barrier and the start (tests inject a
+    start skew there)."""
+    sync()
+    barrier(env)
+    if before_start is not None:
+        before_start()
+    t0 = time.monotonic_ns()
+    for i in range(steps):
+        step(i)
+    sync()
+    t1 = time.monotonic_ns()
+    barrier(env)
+    return t0, t1
+
+
+def aggregate(starts_ns, ends_ns, units, steps: int) -> dict:
+    """SURVEY.md 8e's aggregate over ranks that share one clock: Σ units x steps
+    / (latest end - earliest start).  A rank that starts late after the barrier
+    lengthens the span, so the rate cannot be overstated by start skew; the
+    max-over-ranks elapsed time (each rank's own end - start) is kept beside it."""
+    span = max(ends_ns) - min(starts_ns)
+    own = [e - s for s, e in zip(starts_ns, ends_ns)]
+    total = float(sum(units)) * steps
+    return {"span_s": span / 1e9, "max_rank_s": max(own) / 1e9,
+            "start_skew_ms": (max(starts_ns) - min(starts_ns)) / 1e6,
+            "end_skew_ms": (max(ends_ns) - min(ends_ns)) / 1e6,
+            "rate": total / (span / 1e9), "rate_max_rank": total / (max(own) / 1e9)}
 
 
 def init_control_plane(env: DistEnv) -> None:
@@ -185,6 +227,19 @@ def gather_over_ranks(env: DistEnv, values: list[float]) -> list[list[float]]:
     out = [torch.empty_like(t) for _ in range(env.world)]
     dist.all_gather(out, t)
     return [o.tolist() for o in out]
+
+
+def gather_ints(env: DistEnv, values: list[int]) -> list[list[int]]:
+    """Every rank's int64 ``values`` (exact: clock readings in ns), indexed by rank."""
+    if not env.distributed:
+        return [[int(v) for v in values]]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(values, dtype=torch.int64)
+    out = [torch.empty_like(t) for _ in range(env.world)]
+    dist.all_gather(out, t)
+    return [[int(x) for x in o.tolist()] for o in out]
 
 
 def gather_objects(env: DistEnv, obj) -> list:

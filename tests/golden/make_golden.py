@@ -169,7 +169,10 @@ def sha(a) -> str:
 # zero bytes -> 0xFFFF where there is no pseudo-header (pip_ip_checksum of an
 # all-zero header).  "zero_flows_every": flow records k % zero_flows_every == 0
 # get zero addresses; with proto 0 and length 0 (an empty segment) their total
-# is 0 and pip returns 0xFFFF under a pseudo-header.  Each spec names the batch
+# is 0 and pip returns 0xFFFF under a pseudo-header.  "family": 0 drops the
+# config's pseudo-header (pip_ip_checksum semantics over the whole segment), so
+# all-zero packets fold to pip's ~fold(0) = 0xFFFF (pip/pip_checksum.cpp:29-38)
+# through the jumbo and byte-packed bench kernels too.  Each spec names the batch
 # kernel it exercises (tests/test_gpu_parity.py checks pipck_last_launch).
 EDGES = {
     "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat<24,"},
@@ -180,6 +183,11 @@ EDGES = {
                           "kernel": "k_packedb<"},
     "edge_flat_len0_v4": {"cfg": 2, "n": 256, "stride": 1024, "length": 0, "proto": 0, "zero_flows_every": 4,
                           "kernel": "k_flat<24,"},
+    # no pseudo-header, all-zero packets -> 0xFFFF, self-checksummed ones -> 0x0000
+    "edge_coop_nopseudo_tcp4": {"cfg": 5, "n": 96, "family": 0, "proto": 0, "ck_every": 4, "ck_off": 16,
+                                "zero_every": 3, "kernel": "k_flat_coop<32,"},
+    "edge_packedb_nopseudo": {"cfg": 4, "n": 2048, "family": 0, "proto": 0, "ck_every": 5, "ck_off": 16,
+                              "zero_every": 3, "layout": "bytes", "kernel": "k_packedb<"},
 }
 
 
@@ -201,9 +209,14 @@ def edge_inputs_cpu(orc, b: dict):
         arena = orc.gen_fixed_batch(b["seed"], b["first"], n, L, b["hdr"], st) if L else np.zeros(n * st, np.uint8)
         offs, lens = np.arange(n, dtype=np.uint64) * st, np.full(n, L, dtype=np.uint32)
     for o, hx in b["patches"]:
-        v = bytes.fromhex(hx)
+        v = patch_bytes(hx)
         arena[o:o + len(v)] = np.frombuffer(v, dtype=np.uint8)
     return arena, offs, lens, bytes(flows)
+
+
+def patch_bytes(p) -> bytes:
+    """A fixture patch's bytes: hex text, or an int = that many zero bytes."""
+    return bytes(p) if isinstance(p, int) else bytes.fromhex(p)
 
 
 def oracle_edge_results(orc, b: dict, arena, offs, lens, flows: bytes) -> np.ndarray:
@@ -228,7 +241,7 @@ def edge_batch(orc, ref, name: str, spec: dict) -> dict:
     w = next(x for x in ALL.values() if x.cfg == spec["cfg"])
     n, first = spec["n"], 0
     proto = spec.get("proto", w.proto)
-    fam = w.family
+    fam = spec.get("family", w.family)
     flows = bytearray(orc.flows_table(fam, w.seed, N_FLOWS, proto) if fam else b"")
     rec = 12 if fam == 4 else 36
     zero_flows = list(range(0, N_FLOWS, spec["zero_flows_every"])) if spec.get("zero_flows_every") else []
@@ -258,11 +271,11 @@ def edge_batch(orc, ref, name: str, spec: dict) -> dict:
     for i in range(n):
         o, L = int(offs[i]), int(lens[i])
         if spec.get("zero_every") and i % spec["zero_every"] == 1:
-            patches.append([o, "00" * L])
+            patches.append([o, L])  # an int: a run of L zero bytes
         elif spec.get("ck_every") and i % spec["ck_every"] == 0 and L >= spec["ck_off"] + 2:
             patches.append([o + spec["ck_off"], int(base[i]).to_bytes(2, "big").hex()])
     for o, hx in patches:
-        b = bytes.fromhex(hx)
+        b = patch_bytes(hx)
         arena[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
     out = pip_results(arena)
     rec_ = {"n": n, "first": first, "family": fam, "proto": proto, "n_flows": N_FLOWS}

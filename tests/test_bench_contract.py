@@ -60,7 +60,7 @@ def test_committed_traffic_files_carry_kernel_and_build():
         assert t["kernel"].startswith("void pipck::k_") and "(" in t["kernel"], f.name
 
 
-@pytest.mark.parametrize("world,n_dev,share,ok", [
+@pytest.mark.parametrize("world,n_dev,share,ok", [  # world = ranks on the node
     (1, 1, False, True), (8, 8, False, True), (4, 8, False, True),
     (2, 1, False, False), (8, 1, False, False), (8, 4, False, False),
     (4, 1, True, True), (8, 4, True, True), (1, 0, False, False), (1, 0, True, False),
@@ -122,3 +122,59 @@ class TestPackedBoundsCache:
         engine._check_packed(torch.empty(320, dtype=torch.uint8), lens, tc, 100)
         with pytest.raises(ValueError):
             engine._check_packed(torch.empty(319, dtype=torch.uint8), lens, tc, 100)
+
+
+def test_aggregate_is_span_from_earliest_start_to_latest_end():
+    """Σ units / (max end - min start); a late starter lengthens
+    the span even when every rank's own elapsed time is the same."""
+    ms = 1_000_000
+    even = shard.aggregate([0, 0], [50 * ms, 50 * ms], [1e9, 1e9], 10)
+    assert even["span_s"] == even["max_rank_s"] == 0.05 and even["rate"] == even["rate_max_rank"] == 4e11
+    skewed = shard.aggregate([0, 100 * ms], [50 * ms, 150 * ms], [1e9, 1e9], 10)
+    assert skewed["max_rank_s"] == 0.05 and skewed["span_s"] == 0.15
+    assert skewed["start_skew_ms"] == 100 and skewed["end_skew_ms"] == 100
+    assert skewed["rate"] == pytest.approx(2e10 / 0.15) and skewed["rate_max_rank"] == 4e11
+
+
+_SKEW_SCRIPT = """
+import json, sys, time
+sys.path.insert(0, {root!r})
+from pip_amd import shard
+env = shard.dist_env()
+shard.init_control_plane(env)
+steps, step_s, skew_s = 5, 0.02, {skew}
+t0, t1 = shard.timed_steps(env, steps, lambda i: time.sleep(step_s), lambda: None,
+                           before_start=lambda: time.sleep(env.rank * skew_s))
+clocks = shard.gather_ints(env, [t0, t1])
+agg = shard.aggregate([c[0] for c in clocks], [c[1] for c in clocks], [1e9] * env.world, steps)
+if env.rank == 0:
+    print("AGG " + json.dumps(agg), flush=True)
+shard.shutdown(env)
+"""
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_injected_start_skew_lowers_the_aggregate(tmp_path, capfd, world):
+    """gloo ranks on one host whose timed starts are skewed after the barrier
+    (rank r waits r x 60 ms, as bench.py --start-skew-ms does): the reported
+    aggregate drops by the skew, while the max-over-ranks elapsed time would
+    not see it.  Unskewed, the two agree."""
+    import json
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parents[1])
+    got = {}
+    for skew in (0.0, 0.06):
+        script = tmp_path / f"skew{skew}.py"
+        script.write_text(_SKEW_SCRIPT.format(root=root, skew=skew))
+        assert shard.spawn_ranks(world, [sys.executable, str(script)]) == 0
+        out = capfd.readouterr().out
+        got[skew] = json.loads(next(ln for ln in out.splitlines() if ln.startswith("AGG "))[4:])
+    flat, skewed = got[0.0], got[0.06]
+    want_skew = (world - 1) * 60
+    assert flat["start_skew_ms"] < 30 and flat["span_s"] < flat["max_rank_s"] + 0.03
+    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 40
+    assert skewed["span_s"] >= skewed["max_rank_s"] + (want_skew - 5) / 1e3
+    assert skewed["rate"] < 0.75 * skewed["rate_max_rank"]
+    assert skewed["rate"] == pytest.approx(world * 1e9 * 5 / skewed["span_s"])

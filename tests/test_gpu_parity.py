@@ -23,7 +23,7 @@ torch = pytest.importorskip("torch")
 from pip_amd import _lib, engine  # noqa: E402
 from pip_amd import checksum as pc  # noqa: E402
 from pip_amd.workloads import ALL, CFG1, CFG2, CFG3, CFG4, CFG5, N_FLOWS  # noqa: E402
-from tests.golden.make_golden import run_case  # noqa: E402
+from tests.golden.make_golden import patch_bytes, run_case  # noqa: E402
 
 DEV = "cuda"
 
@@ -246,7 +246,7 @@ def test_edge_fixture_through_batch_kernel(batches, name):
     else:
         arena = torch.zeros(n * b["stride"], dtype=torch.uint8, device=DEV)
     for o, hx in b["patches"]:
-        v = bytes.fromhex(hx)
+        v = patch_bytes(hx)
         arena[o:o + len(v)] = torch.frombuffer(bytearray(v), dtype=torch.uint8).to(DEV)
     assert sha(arena.cpu().numpy()) == b["arena_sha256"]
     pseudo = None
@@ -395,6 +395,8 @@ def test_flat_coop_kernel_vs_oracle(oracle, ring, rows):
             host = rng.integers(0, 256, n * stride, dtype=np.uint8)
             if n > 2:
                 host[stride:2 * stride] = 0xFF
+            if n > 3:
+                host[3 * stride:4 * stride] = 0  # all zero: 0xFFFF without a pseudo-header
             _, arena = upload(host, 0)
             fam = int(rng.choice([0, 4, 6]))
             seed, proto, origin = int(rng.integers(0, 2**62)), 6, int(rng.integers(0, 3000))
@@ -403,6 +405,8 @@ def test_flat_coop_kernel_vs_oracle(oracle, ring, rows):
             assert "k_flat_coop<" in last_kernel()
             want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
             assert np.array_equal(got, want), (stride, length, n, np.nonzero(got != want)[0][:5])
+            if n > 3 and not fam:
+                assert got[3] == 0xFFFF  # pip's ~fold(0) (pip_checksum.cpp:29-38)
             ok = engine.verify_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin).cpu().numpy()
             assert np.array_equal(ok.astype(bool), got == 0)
     finally:

@@ -180,6 +180,26 @@ def test_bench_two_ranks_json_contract():
     assert d["config"]["global_packets"] == 400000 and d["config"]["packets_per_gpu"] == 200000
     assert d["value"] > 0 and d["roofline"]["bound"] == "hbm" and d["cpu_baseline"] is None
     assert len(d["per_rank_gib_per_s"]) == 2
+    # value over the span from the earliest start to the latest end
+    t = d["timing"]
+    assert t["value_over"].startswith("latest end - earliest start")
+    assert t["span_ms"] >= t["max_rank_elapsed_ms"] and t["start_skew_ms"] >= 0
+    assert d["value"] <= t["value_by_max_rank_elapsed"] + 0.01
+    assert d["ms_per_step"] == pytest.approx(t["span_ms"] / 3, rel=1e-3)
+
+
+def test_bench_start_skew_lowers_the_value():
+    """An injected start skew after the barrier (rank 1 starts 200 ms late) shows
+    in the line: start_skew_ms, and a value below the max-rank-elapsed figure."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--packets-per-gpu", "200000", "--no-cpu", "--start-skew-ms", "200", *share_flag(2)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    t = d["timing"]
+    assert 190 < t["start_skew_ms"] < 400 and t["injected_start_skew_ms_per_rank"] == 200
+    assert t["span_ms"] >= t["max_rank_elapsed_ms"] + 190
+    assert d["value"] < 0.5 * t["value_by_max_rank_elapsed"]
 
 
 def test_bench_cfg4_two_ranks_byte_split():

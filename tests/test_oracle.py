@@ -103,6 +103,10 @@ def test_edge_fixtures_cover_both_corners(batches):
     # and 0x0000 through every batch kernel family the bench runs
     kernels = {b["kernel"] for b in edges if b["n_zero"]}
     assert {"k_flat<24,", "k_flat_coop<32,", "k_small<", "k_packed<", "k_packedb<"} <= kernels
+    # and 0xFFFF (pip's ~fold(0), pip_checksum.cpp:29-38) through the jumbo and
+    # byte-packed bench kernels, from all-zero packets with no pseudo-header
+    ffff = {b["kernel"] for b in edges if b["n_ffff"] and not b["family"]}
+    assert {"k_flat_coop<32,", "k_packedb<", "k_small<"} <= ffff
 
 
 def test_zipf_shape(oracle):
