@@ -122,6 +122,20 @@ int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uin
 int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
                         uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                         uint64_t flow_origin, uint8_t* d_ok, void* stream);
+/* Bounded forms: arena_bytes = the arena's size (readable up to the 16-byte
+ * boundary at or above it).  A tile of 64 packets whose chunks, as d_tile_chunk
+ * and d_lens place them, reach past the arena -- a stale or foreign index --
+ * is not read at all: each of its packets gets 0 (d_ok 0) and d_err (optional,
+ * device u32) is OR-ed with (1 << PIPCK_ERANGE).  The plain names above trust
+ * the index (arena_bytes unbounded). */
+int pipck_checksum_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                            const uint64_t* d_tile_chunk, uint64_t n_packets, const uint32_t* d_pseudo,
+                            uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
+                            uint32_t* d_err, void* stream);
+int pipck_verify_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                          const uint64_t* d_tile_chunk, uint64_t n_packets, const uint32_t* d_pseudo,
+                          uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok,
+                          uint32_t* d_err, void* stream);
 /* Build d_tile_chunk (ceil(n/64) + 1 u64 entries; the last = the arena's 16-byte
  * chunks) from the lengths, on the stream. */
 int pipck_packed_index(const uint16_t* d_lens, uint64_t n_packets, uint64_t* d_tile_chunk, void* stream);
@@ -143,6 +157,17 @@ int pipck_checksum_packed_bytes(const void* d_arena, const uint16_t* d_lens, con
 int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off,
                               uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows,
                               const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok, void* stream);
+/* Bounded forms, as pipck_checksum_packed_n: a tile whose bytes reach past
+ * arena_bytes (readable to the 16-byte boundary at or above it) is not read;
+ * its packets get 0 and d_err gets (1 << PIPCK_ERANGE). */
+int pipck_checksum_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                                  const uint64_t* d_tile_off, uint64_t n_packets, const uint32_t* d_pseudo,
+                                  uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
+                                  uint32_t* d_err, void* stream);
+int pipck_verify_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                                const uint64_t* d_tile_off, uint64_t n_packets, const uint32_t* d_pseudo,
+                                uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok,
+                                uint32_t* d_err, void* stream);
 int pipck_packed_bytes_index(const uint16_t* d_lens, uint64_t n_packets, uint64_t* d_tile_off, void* stream);
 
 /* Chains (pip_buf lists, pip_checksum.cpp:90-148): packet p owns segments

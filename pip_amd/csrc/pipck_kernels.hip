@@ -1255,7 +1255,8 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
                                                const uint64_t* __restrict__ tile_chunk, uint64_t n,
                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                                               uint64_t arena_chunks, uint32_t* __restrict__ err) {
     __shared__ RaggedTileLds t;
     const int lane = threadIdx.x & 63;
     const uint64_t tile = blockIdx.x;
@@ -1274,8 +1275,23 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
     // zeroed, and packet 0 of the tile is streamed as if it began there, so
     // every 1 KiB row is 8 whole lines and no line is fetched by two rows of a
     // tile (tune flags bit 30: the r02 grid from the tile's first chunk).
-    const uintptr_t tbase = (uintptr_t)arena + 16ull * tile_chunk[tile];
     const uint32_t nch = (len + 15) >> 4;
+    const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
+    // The tile's chunks [tc0, tc0 + its chunk count) must lie in the arena
+    // (scalar, overflow-safe): a tile reaching past it -- a stale or foreign
+    // index -- reads nothing, sets PIPCK_ERANGE in err and yields 0 for each of
+    // its packets.
+    const uint64_t tc0 = tile_chunk[tile];
+    const uint32_t tile_ch = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(nch), 63);
+    if (!(tc0 <= arena_chunks && (uint64_t)tile_ch <= arena_chunks - tc0)) {
+        if (lane == 0 && err) atomicOr(err, 1u << PIPCK_ERANGE);
+        if (VERIFY)
+            store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, 0u);
+        else
+            store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, 0u);
+        return;
+    }
+    const uintptr_t tbase = (uintptr_t)arena + 16ull * tc0;
     const uint32_t lead = (__all(nch <= kTinyChunks) || (kflags & kPackedNoAlign)) ? 0u : (uint32_t)(tbase >> 4) & 7u;
     const uint32_t nch_s = nch + (lane == 0 ? lead : 0u);
     const uint32_t excl = wave_incl_scan(nch_s) - nch_s;
@@ -1286,7 +1302,6 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
     const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
     const uint32_t P = pseudo ? Pbase + len : 0u;
     const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
-    const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
     if (kflags & kPlainResultStores) {
         if (valid) {
             if (VERIFY)
@@ -1729,25 +1744,26 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
 template <bool V, int U>
 static void launch_packed_u(bool nt, uint64_t tiles, hipStream_t s, const uint8_t* a, const uint16_t* lens,
                             const uint64_t* tc, uint64_t n, const uint32_t* ps, uint32_t nf, const uint32_t* fo,
-                            uint64_t origin, uint16_t* out, uint8_t* ok, uint32_t f) {
+                            uint64_t origin, uint16_t* out, uint8_t* ok, uint32_t f, uint64_t ach, uint32_t* err) {
     const bool marks = (f & kPackedMarksOnly) != 0;
     if (nt && marks)
         PIPCK_LAUNCH((k_packed<V, U, true, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
-                           fo, origin, out, ok, f);
+                           fo, origin, out, ok, f, ach, err);
     else if (nt)
         PIPCK_LAUNCH((k_packed<V, U, true, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
-                           fo, origin, out, ok, f);
+                           fo, origin, out, ok, f, ach, err);
     else if (marks)
         PIPCK_LAUNCH((k_packed<V, U, false, true>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
-                           fo, origin, out, ok, f);
+                           fo, origin, out, ok, f, ach, err);
     else
         PIPCK_LAUNCH((k_packed<V, U, false, false>), dim3((uint32_t)tiles), dim3(64), 0, s, a, lens, tc, n, ps, nf,
-                           fo, origin, out, ok, f);
+                           fo, origin, out, ok, f, ach, err);
 }
 
-static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
-                         uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
-                         uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, hipStream_t s) {
+static int launch_packed(bool verify, const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                         const uint64_t* d_tile_chunk, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                         const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok,
+                         uint32_t* d_err, hipStream_t s) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_lens || !d_tile_chunk || (verify ? !d_ok : !d_out)) {
         set_error("pipck_checksum_packed: null pointer");
@@ -1766,6 +1782,8 @@ static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_len
         set_error("pipck_checksum_packed: more than 2^37 packets in one launch");
         return PIPCK_ERANGE;
     }
+    // whole 16-byte chunks the kernel may read: the arena's bytes rounded up to 16
+    const uint64_t ach = arena_bytes / 16 + (arena_bytes % 16 ? 1u : 0u);
     // Mixed rows take the LDS-marks path by default here (tune flags bit 19
     // selects the scalar end loop instead, the reverse of k_ragged), with a
     // ring of 32 rows (154 VGPRs, still 3 waves/SIMD): cfg4 1.2618 vs 1.2814 ms and, at 16M
@@ -1777,14 +1795,14 @@ static int launch_packed(bool verify, const void* d_arena, const uint16_t* d_len
     const uint32_t nf = n_flows ? n_flows : 1u;
     // rows in flight per wave: 17/25/33 = rings of 16/24/32
     switch (g_tune.loads.load()) {
-        case 17: verify ? launch_packed_u<true, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
-                        : launch_packed_u<false, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+        case 17: verify ? launch_packed_u<true, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err)
+                        : launch_packed_u<false, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err);
                  break;
-        case 25: verify ? launch_packed_u<true, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
-                        : launch_packed_u<false, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+        case 25: verify ? launch_packed_u<true, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err)
+                        : launch_packed_u<false, 24>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err);
                  break;
-        default: verify ? launch_packed_u<true, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f)
-                        : launch_packed_u<false, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f);
+        default: verify ? launch_packed_u<true, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err)
+                        : launch_packed_u<false, 32>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err);
                  break;
     }
     PIPCK_LAUNCHED("k_packed");
@@ -1910,18 +1928,35 @@ int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t 
     return launch_ragged(true, d_arena, d_desc, n, d_pseudo, nullptr, nullptr, d_ok, d_err, as_stream(stream));
 }
 
+int pipck_checksum_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                            const uint64_t* d_tile_chunk, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                            const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint32_t* d_err,
+                            void* stream) {
+    return launch_packed(false, d_arena, arena_bytes, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                         flow_origin, d_out, nullptr, d_err, as_stream(stream));
+}
+
+int pipck_verify_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                          const uint64_t* d_tile_chunk, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                          const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok, uint32_t* d_err,
+                          void* stream) {
+    return launch_packed(true, d_arena, arena_bytes, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                         flow_origin, nullptr, d_ok, d_err, as_stream(stream));
+}
+
+// the unbounded forms (the index is trusted): every tile's chunks must lie in the arena
 int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
                           const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
                           uint16_t* d_out, void* stream) {
-    return launch_packed(false, d_arena, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out,
-                         nullptr, as_stream(stream));
+    return pipck_checksum_packed_n(d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                                   flow_origin, d_out, nullptr, stream);
 }
 
 int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
                         const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
                         uint8_t* d_ok, void* stream) {
-    return launch_packed(true, d_arena, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr,
-                         d_ok, as_stream(stream));
+    return pipck_verify_packed_n(d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                                 flow_origin, d_ok, nullptr, stream);
 }
 
 int pipck_packed_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_chunk, void* stream) {

@@ -163,7 +163,8 @@ __global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ aren
                                                 const uint64_t* __restrict__ tile_off, uint64_t n,
                                                 const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                 const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                uint64_t arena_bytes, uint32_t* __restrict__ err) {
     __shared__ PackedbLds t;
     const int lane = threadIdx.x & 63;
     const uint64_t tile = blockIdx.x;
@@ -176,9 +177,25 @@ __global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ aren
         Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
     }
     const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
-    const uint64_t first = (uint64_t)(uintptr_t)arena + tile_off[tile];
+    const uint32_t incl = wave_incl_scan(len);
+    // The tile's bytes [toff, toff + its lengths) must lie in the arena (scalar,
+    // overflow-safe): a tile reaching past arena_bytes -- a stale or foreign
+    // index -- reads nothing, sets PIPCK_ERANGE in err and yields 0 for each of
+    // its packets, so a wrong index can never take the loads outside the arena.
+    const uint64_t toff = tile_off[tile];
+    const uint32_t tile_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const bool in_arena = toff <= arena_bytes && (uint64_t)tile_len <= arena_bytes - toff;
+    if (!in_arena) {
+        if (lane == 0 && err) atomicOr(err, 1u << PIPCK_ERANGE);
+        if (VERIFY)
+            store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, 0u);
+        else
+            store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, 0u);
+        return;
+    }
+    const uint64_t first = (uint64_t)(uintptr_t)arena + toff;
     const uintptr_t base = (uintptr_t)(first & ~127ull);  // the line holding the tile's first byte
-    const uint32_t excl = wave_incl_scan(len) - len;
+    const uint32_t excl = incl - len;
     const uint32_t start = (uint32_t)(first - base) + excl;  // relative to base
     const uint32_t end = start + len;
     const uint32_t end_last = (uint32_t)__builtin_amdgcn_readlane((int)end, (int)(nv - 1));
@@ -242,9 +259,10 @@ __global__ __launch_bounds__(1024) void k_packedb_tile_scan(uint64_t* __restrict
     if (i == 0) tile_off[0] = 0;
 }
 
-static int launch_packedb(bool verify, const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off,
-                          uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
-                          uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, hipStream_t s) {
+static int launch_packedb(bool verify, const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                          const uint64_t* d_tile_off, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                          const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok,
+                          uint32_t* d_err, hipStream_t s) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_lens || !d_tile_off || (verify ? !d_ok : !d_out)) {
         set_error("pipck_checksum_packed_bytes: null pointer");
@@ -268,11 +286,11 @@ static int launch_packedb(bool verify, const void* d_arena, const uint16_t* d_le
     if (verify)
         PIPCK_LAUNCH((k_packedb<true, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
                           (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
-                          d_ok);
+                          d_ok, arena_bytes, d_err);
     else
         PIPCK_LAUNCH((k_packedb<false, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
                           (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
-                          d_ok);
+                          d_ok, arena_bytes, d_err);
     PIPCK_LAUNCHED("k_packedb");
     return PIPCK_OK;
 }
@@ -283,18 +301,35 @@ using namespace pipck;
 
 extern "C" {
 
+int pipck_checksum_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                                  const uint64_t* d_tile_off, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                                  const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint32_t* d_err,
+                                  void* stream) {
+    return launch_packedb(false, d_arena, arena_bytes, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                          flow_origin, d_out, nullptr, d_err, as_stream(stream));
+}
+
+int pipck_verify_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                                const uint64_t* d_tile_off, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
+                                const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok, uint32_t* d_err,
+                                void* stream) {
+    return launch_packedb(true, d_arena, arena_bytes, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                          flow_origin, nullptr, d_ok, d_err, as_stream(stream));
+}
+
+// the unbounded forms (the index is trusted): every tile's bytes must lie in the arena
 int pipck_checksum_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
                                 const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                                 uint64_t flow_origin, uint16_t* d_out, void* stream) {
-    return launch_packedb(false, d_arena, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out,
-                          nullptr, as_stream(stream));
+    return pipck_checksum_packed_bytes_n(d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                                         flow_origin, d_out, nullptr, stream);
 }
 
 int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
                               const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                               uint64_t flow_origin, uint8_t* d_ok, void* stream) {
-    return launch_packedb(true, d_arena, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr,
-                          d_ok, as_stream(stream));
+    return pipck_verify_packed_bytes_n(d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                                       flow_origin, d_ok, nullptr, stream);
 }
 
 int pipck_packed_bytes_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_off, void* stream) {

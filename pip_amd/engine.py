@@ -128,29 +128,35 @@ def verify_ragged(arena, desc, pseudo=None, ok=None, err=None):
     return ok
 
 
+def _nbytes(t) -> int:
+    return t.numel() * t.element_size()
+
+
 def checksum_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                    flow_origin: int = 0, out=None):
-    """Packed ragged batch (pipck_checksum_packed): lens = device int16/uint16 tensor of
-    packet lengths, tile_chunk = packed_index(lens); packet i at 16 * (chunks before i)."""
+                    flow_origin: int = 0, out=None, err=None):
+    """Packed ragged batch (pipck_checksum_packed_n): lens = device int16/uint16 tensor of
+    packet lengths, tile_chunk = packed_index(lens); packet i at 16 * (chunks before i).
+    The device bounds every tile by the arena's size (err: optional device int32,
+    OR-ed with 1 << PIPCK_ERANGE for a tile past it, whose results are then 0)."""
     torch = _torch()
     n = lens.numel() if n is None else n
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_packed(arena, lens, tile_chunk, n)
-    call("pipck_checksum_packed", _ptr(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo), n_flows, _ptr(flow_of),
-         flow_origin, _ptr(out), current_stream(arena.device))
+    call("pipck_checksum_packed_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo),
+         n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
     return out
 
 
 def verify_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                  flow_origin: int = 0, ok=None):
+                  flow_origin: int = 0, ok=None, err=None):
     torch = _torch()
     n = lens.numel() if n is None else n
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
     _check_packed(arena, lens, tile_chunk, n)
-    call("pipck_verify_packed", _ptr(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo), n_flows, _ptr(flow_of),
-         flow_origin, _ptr(ok), current_stream(arena.device))
+    call("pipck_verify_packed_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo),
+         n_flows, _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err), current_stream(arena.device))
     return ok
 
 
@@ -167,7 +173,8 @@ _packed_total: dict = {}  # id(tile_chunk) -> (weakref, tensor version, n, chunk
 
 
 def _check_packed(arena, lens, tile_chunk, n, unit: int = 16):
-    """Host-side guard: the batch must lie inside the arena.  The index's total
+    """Host-side guard (the device bounds every tile as well, pipck_*_packed*_n):
+    the batch must lie inside the arena.  The index's total
     (tile_chunk[ceil(n/64)], one device read) is cached on the index tensor
     OBJECT and its in-place version counter, never on addresses: a freed tensor's
     address is reused by the caching allocator, and a pointer-keyed cache would
@@ -191,28 +198,29 @@ def _check_packed(arena, lens, tile_chunk, n, unit: int = 16):
 
 
 def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                          flow_origin: int = 0, out=None):
-    """Byte-packed ragged batch (pipck_checksum_packed_bytes): packets back to back with no padding,
-    lens = device int16/uint16 lengths, tile_off = packed_bytes_index(lens); arena 128-byte aligned."""
+                          flow_origin: int = 0, out=None, err=None):
+    """Byte-packed ragged batch (pipck_checksum_packed_bytes_n): packets back to back with no padding,
+    lens = device int16/uint16 lengths, tile_off = packed_bytes_index(lens); arena 128-byte aligned.
+    Tiles are bounded by the arena's size on the device (err as checksum_packed)."""
     torch = _torch()
     n = lens.numel() if n is None else n
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_packed(arena, lens, tile_off, n, unit=1)
-    call("pipck_checksum_packed_bytes", _ptr(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo), n_flows,
-         _ptr(flow_of), flow_origin, _ptr(out), current_stream(arena.device))
+    call("pipck_checksum_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo),
+         n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
     return out
 
 
 def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                        flow_origin: int = 0, ok=None):
+                        flow_origin: int = 0, ok=None, err=None):
     torch = _torch()
     n = lens.numel() if n is None else n
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
     _check_packed(arena, lens, tile_off, n, unit=1)
-    call("pipck_verify_packed_bytes", _ptr(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo), n_flows,
-         _ptr(flow_of), flow_origin, _ptr(ok), current_stream(arena.device))
+    call("pipck_verify_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo),
+         n_flows, _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err), current_stream(arena.device))
     return ok
 
 
