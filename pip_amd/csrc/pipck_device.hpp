@@ -90,7 +90,9 @@ __device__ __forceinline__ uint32_t be_fold(uint32_t le_residue_sum, uintptr_t s
 // identical to the flat variants' (u16)len (:91) inside the batch domain.
 __device__ __forceinline__ uint32_t len_term(uint32_t len) { return (len >> 16) + (len & 0xFFFFu); }
 
-// ~(u16)fold(fold(P + F)) -- pip_checksum.cpp:95/:121/:149/:182
+// ~(u16)fold(fold(P + F)) -- the two folds of pip_standard_checksum
+// (pip_checksum.cpp:29-30) and the final ~ of pip_inet_checksum (:60),
+// pip_inet6_checksum (:86), pip_inet_checksum_buf (:114), pip_inet6_checksum_buf (:147)
 __device__ __forceinline__ uint16_t finish(uint32_t pseudo_total, uint32_t be_sum) {
     return (uint16_t)~fold16(pseudo_total + be_sum);
 }

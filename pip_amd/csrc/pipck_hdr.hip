@@ -38,6 +38,12 @@ namespace pipck {
 constexpr uint32_t kHdrPlainStores = 1u << 29;
 constexpr uint32_t kHdrNtStores = 1u << 30;
 constexpr uint32_t kHdrNarrowStores = 1u << 31;
+// bit 28, measurement only: store each header's checksum
+// INTO the header -- htons(result) at byte 10, its ip_sum, as pip_netif.cpp:97
+// stores it -- instead of into the result array (which is left untouched): the
+// "results inside the headers" layout, to weigh its write-back of whole dirty
+// lines against the separate 2-byte result stream.
+constexpr uint32_t kHdrInPlace = 1u << 28;
 
 template <int D>
 struct HdrGeom {
@@ -118,6 +124,14 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
         }
     }
     wave_sync();
+    if (!VERIFY && (kflags & kHdrInPlace)) {  // measurement: results into the headers' ip_sum
+        const buf_t hb = buf_rsrc(arena + b0, (uint32_t)((uint64_t)np * (4u * D)));
+        for (uint32_t i = lane; i < np; i += 64) {
+            const uint32_t r = res[i];
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((r >> 8) | (r << 8)), hb, (int)(i * 4u * D + 10u), 0, 0);
+        }
+        return;
+    }
     // the task's results, contiguous from out + p0 (ok + p0): whole 16-byte
     // pieces as one b128 store per lane (a full task of 3,072 headers is 6 KiB
     // = 6 store instructions), the rest one result per lane

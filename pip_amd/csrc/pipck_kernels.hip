@@ -260,6 +260,31 @@ constexpr uint32_t kTrace = 1u << 20;
 struct TaskTrace {
     uint64_t task, t0, t1, hw;  // hw = XCC_ID << 32 | HW_ID
 };
+// XCD-weighted static deal (k_flat_xw; pipck_tune_xcd_weights in pipck_testing.h).
+// The dispatcher deals block b to XCD b % 8, so every XCD gets an eighth of a
+// launch's blocks whatever its HBM rate.  Here the grid is cut into periods of
+// 8 M blocks, and in each period XCD x keeps only its first m_x blocks; the
+// others exit at once.  The kept blocks take consecutive virtual block numbers
+// in dispatch order, so the tasks in flight stay one contiguous window, and a
+// faster XCD (larger m_x) takes a larger share of the tasks.
+__device__ uint32_t g_xw[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // m_0 .. m_7, M
+struct VBlock {
+    uint64_t b, grid;  // virtual block number and virtual grid (kept blocks)
+    bool live;
+};
+__device__ __forceinline__ VBlock xw_block() {
+    const uint32_t M = g_xw[8];
+    uint32_t A = 0;
+#pragma unroll
+    for (int x = 0; x < 8; x++) A += g_xw[x];
+    const uint32_t P = 8u * M, j = blockIdx.x % P, x = j & 7u, i = j >> 3;
+    uint32_t before = 0;  // kept blocks of this period dispatched before block j
+#pragma unroll
+    for (int y = 0; y < 8; y++) before += min(g_xw[y], i) + ((uint32_t)y < x && i < g_xw[y] ? 1u : 0u);
+    const uint64_t periods = gridDim.x / P;
+    return {(uint64_t)(blockIdx.x / P) * A + before, periods * A, i < g_xw[x]};
+}
+
 __device__ TaskTrace* g_trace = nullptr;
 __device__ uint64_t g_trace_cap = 0;
 
@@ -488,12 +513,22 @@ constexpr int flat_waves_per_simd() { return U >= 32 ? 2 : (U >= 24 ? 3 : (U >= 
 // The kernel body; PROBE = false compiles the measurement-only bits (21-23)
 // out of the production kernel k_flat (no per-row flag test), and k_flat_probe
 // keeps them for the tools.
-template <int U, bool PIPE, bool VERIFY, bool NT, int WPB, bool PROBE>
+template <int U, bool PIPE, bool VERIFY, bool NT, int WPB, bool PROBE, bool XW = false>
 __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __restrict__ arena, uint32_t cpp,
                                           uint32_t len, uint64_t n, uint32_t run, const uint32_t* __restrict__ pseudo,
                                           uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
                                           uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
     if (!PROBE) kflags &= ~(kLoadsOnly | kNoTaskEnd | kEndNoStore);
+    // the block's place in the task order: its own number, or (XW) its number
+    // among the blocks the XCD-weighted deal keeps
+    uint64_t vb = blockIdx.x, vgrid = gridDim.x;
+    if (XW) {
+        const VBlock v = xw_block();
+        if (!v.live) return;  // block-uniform, before any barrier
+        vb = v.b;
+        vgrid = v.grid;
+        kflags &= ~kXcdGroups;
+    }
     const int lane = threadIdx.x & 63;
     const uint32_t pitch = flat_pitch(run);
     uint16_t* part = s_part + (threadIdx.x >> 6) * 64u * pitch;
@@ -501,7 +536,9 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     const uint32_t lterm = len_term(len);
     const uint64_t n_tasks = (n + run - 1) / run;
-    const TaskRange tr = xcd_tasks<WPB>(n_tasks, (kflags & kXcdGroups) != 0);
+    const TaskRange tr = XW ? TaskRange{vb * WPB + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)),
+                                        n_tasks, vgrid * WPB}
+                            : xcd_tasks<WPB>(n_tasks, (kflags & kXcdGroups) != 0);
     const TraceBuf trb = trace_buf(kflags);
     // Block-coalesced result stores (the default; needs one task per wave and
     // the block's waves on consecutive tasks): each wave parks its packets'
@@ -512,7 +549,7 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
     // cfg5 1.5 % -- as much as the whole task end -- while the same stores all
     // aimed at one line cost nothing (profiles/r03_flat_end_probe.jsonl).  With
     // run a multiple of 16 (launch_fixed) a block's results are whole lines.
-    const bool coalesce = !(kflags & (kFlatWaveStores | kXcdGroups)) && (uint64_t)gridDim.x * WPB >= n_tasks;
+    const bool coalesce = !(kflags & (kFlatWaveStores | kXcdGroups)) && vgrid * WPB >= n_tasks;
     uint16_t* bres = s_part + WPB * 64u * pitch;                       // WPB * run u16
     uint32_t* bcnt = reinterpret_cast<uint32_t*>(bres + ((WPB * run + 1u) & ~1u));
     if (coalesce) {
@@ -585,9 +622,11 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
             uint32_t prev = 0;
             if (lane == 0) prev = atomicAdd(bcnt, 1u);
             prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
-            const uint64_t t0 = (uint64_t)blockIdx.x * WPB;
+            const uint64_t t0 = vb * WPB;
             const uint32_t active = (uint32_t)min<uint64_t>(WPB, n_tasks - t0);
-            if (prev + 1 == active) {
+            // measurement bit 23 (probe kernel only): the results are computed and
+            // parked in LDS, and no wave stores them
+            if (prev + 1 == active && !(PROBE && (kflags & kEndNoStore))) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 const uint64_t q0 = t0 * run;
                 const uint32_t cnt = (uint32_t)min<uint64_t>((uint64_t)WPB * run, n - q0);
@@ -623,6 +662,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_w
     extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16 (launch_fixed sizes it)
     flat_body<U, PIPE, VERIFY, NT, WPB, false>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of, flow_origin,
                                                out, ok, kflags);
+}
+
+// k_flat under the XCD-weighted static deal (xw_block; measurement arm, tools only)
+template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_xw(
+    const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
+    const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    extern __shared__ uint16_t s_part[];
+    flat_body<U, PIPE, VERIFY, NT, WPB, false, true>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of,
+                                                     flow_origin, out, ok, kflags);
 }
 
 // k_flat with the measurement bits 21-23 live (tools only)
@@ -1458,6 +1508,10 @@ static const SmallVariant& small_variant() {
 constexpr uint32_t kNoFlatSmall = 128u;
 constexpr uint64_t kHdrMinBatch = 8ull << 20;  // headers: k_hdr from here, k_small below  // pipck_tune flags bit 7: never the short-stride flat kernel
 
+// host copies of the XCD-weighted deal's shape (pipck_tune_xcd_weights): kept
+// blocks per period (0 = off) and blocks per XCD per period
+static std::atomic<uint32_t> g_xw_kept{0}, g_xw_period{0};
+
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
@@ -1592,6 +1646,16 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const size_t lds = (4u * 64u * flat_pitch(run) + ((4u * run + 1u) & ~1u)) * sizeof(uint16_t) + 16u;
         // the measurement bits (21-23) run k_flat_probe; the production kernel has them compiled out
         const bool probe = (flags & (kLoadsOnly | kNoTaskEnd | kEndNoStore)) && fv->probe && !verify && nt_for(true);
+        // the XCD-weighted deal (pipck_tune_xcd_weights): ring 24, checksum, nt loads
+        const uint32_t xa = g_xw_kept.load();
+        if (xa && !probe && !verify && nt_for(true) && fv->u == 24 && fv->pipe && grid >= 8) {
+            const uint64_t P = 8ull * g_xw_period.load(), periods = (grid + xa - 1) / xa;
+            PIPCK_LAUNCH((k_flat_xw<24, true, false, true>), dim3((uint32_t)(periods * P)), dim3(256), lds,
+                         as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
+                         n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+            PIPCK_LAUNCHED("k_flat_xw");
+            return PIPCK_OK;
+        }
         PIPCK_LAUNCH(probe ? fv->probe : fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
                            (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
                            flow_origin, d_out, d_ok, flags);
@@ -1860,6 +1924,25 @@ int pipck_last_launch(char* buf, size_t cap) {
     std::free(dem);
     if (rc) set_error("pipck_last_launch: buffer too small");
     return rc;
+}
+
+int pipck_tune_xcd_weights(const uint32_t* m, uint32_t period) {
+    uint32_t w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t kept = 0;
+    if (m && period) {
+        if (period > 4096) return PIPCK_EINVAL;
+        for (int x = 0; x < 8; x++) {
+            if (m[x] > period) return PIPCK_EINVAL;
+            w[x] = m[x];
+            kept += m[x];
+        }
+        if (!kept) return PIPCK_EINVAL;
+        w[8] = period;
+    }
+    PIPCK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_xw), w, sizeof w));
+    g_xw_period.store(w[8]);
+    g_xw_kept.store(kept);
+    return PIPCK_OK;
 }
 
 int pipck_trace_tasks(void* d_buf, uint64_t cap) {

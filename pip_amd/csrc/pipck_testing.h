@@ -64,6 +64,13 @@ extern "C" {
  * write-through sc1), 31 = one store per result instead of 16-byte pieces. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
 
+/* XCD-weighted static deal for k_flat (ring 24, checksum; measurement arm,
+ * VERDICT r03 item 7): the grid is cut into periods of 8 x period blocks and
+ * in each XCD x (blocks b with b % 8 == x) keeps its first m[x] blocks; the kept
+ * blocks take the tasks in dispatch order.  m = NULL or period = 0 switches it
+ * off.  Same results; only the share of tasks per XCD changes. */
+int pipck_tune_xcd_weights(const uint32_t* m, uint32_t period);
+
 /* Per-task timeline for tools/task_trace.py: with tune flags bit 20 set, the
  * flat-stream (k_flat) and packed ragged (k_packed) kernels store one record
  * {u64 task, u64 t_start, u64 t_end, u64 XCC_ID << 32 | HW_ID} per wave task

@@ -128,6 +128,13 @@ def verify_ragged(arena, desc, pseudo=None, ok=None, err=None):
     return ok
 
 
+def tune_xcd_weights(m=None, period: int = 0) -> None:
+    """k_flat's XCD-weighted static deal (pipck_tune_xcd_weights, internal): XCD x keeps
+    m[x] of every `period` blocks dealt to it; None / 0 = off."""
+    arr = (C.c_uint32 * 8)(*[int(x) for x in m]) if m is not None else None
+    call("pipck_tune_xcd_weights", arr, period)
+
+
 def _nbytes(t) -> int:
     return t.numel() * t.element_size()
 
@@ -179,7 +186,10 @@ def _check_packed(arena, lens, tile_chunk, n, unit: int = 16):
     OBJECT and its in-place version counter, never on addresses: a freed tensor's
     address is reused by the caching allocator, and a pointer-keyed cache would
     then skip the check for a larger batch.  The bound itself is re-checked
-    against the arena on every call."""
+    against the arena on every call.  An index refilled through a raw pointer
+    (a custom kernel writing into a reused tile_off) does not bump _version, so
+    this guard can keep its old total; the device bound (the _n calls) still
+    refuses every tile past the arena (PIPCK_ERANGE, results 0)."""
     import weakref
 
     if n > lens.numel() or tile_chunk.numel() < (n + 63) // 64 + 1:
@@ -341,10 +351,11 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          trace: bool = False, loads_only: bool = False, no_task_end: bool = False,
          end_no_store: bool = False, alt_flat_schedule: bool = False,
          plain_result_stores: bool = False, wave_stores: bool = False, free_run: bool = False,
-         packed_no_align: bool = False) -> None:
+         packed_no_align: bool = False, hdr_in_place: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
-    except the measurement-only probes loads_only (bit 21), no_task_end (22) and end_no_store (23)."""
+    except the measurement-only probes loads_only (bit 21), no_task_end (22), end_no_store (23) and
+    hdr_in_place (bit 28 read by k_hdr: results into the headers' ip_sum, the result array untouched)."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
@@ -352,7 +363,7 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
              | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0) | (1 << 22 if no_task_end else 0)
-             | (1 << 23 if end_no_store else 0) | (1 << 28 if alt_flat_schedule else 0)
+             | (1 << 23 if end_no_store else 0) | (1 << 28 if (alt_flat_schedule or hdr_in_place) else 0)
              | (1 << 29 if plain_result_stores else 0) | (1 << 30 if (wave_stores or packed_no_align) else 0)
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
