@@ -25,7 +25,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 WORKLOADS = {"cfg1": 256 << 20, "cfg1p": 256 << 20, "cfg2": 4 << 20, "cfg3": 1 << 20, "cfg5": 8 << 20, "cfg4": 8 << 20,
-             "cfg4d": 8 << 20}
+             "cfg4d": 8 << 20, "cfg4b": 8 << 20}
 
 
 def worker(only: list[str], iters: int) -> None:
@@ -45,10 +45,25 @@ def worker(only: list[str], iters: int) -> None:
         w, n = BY_CFG[int(name[3:4])], WORKLOADS[name]
         fam = w.family or (4 if name.endswith("p") else 0)  # cfg1p: cfg1 with IPv4 pseudo-headers
         pseudo = engine.gen_flows(fam, N_FLOWS, w.seed, w.proto or 6)[1] if fam else None
-        if w.ragged and not name.endswith("d"):  # cfg4: the packed layout bench.py runs
+        if name == "cfg4b":  # cfg4 byte-packed: the layout bench.py runs (k_packedb)
+            arena, lens16, tile_off, lens = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+            nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
+            out = torch.empty(n, dtype=torch.int16, device="cuda")
+
+            def run():  # the plain entry point: present in every build under A/B
+                engine.call("pipck_checksum_packed_bytes", engine._ptr(arena), engine._ptr(lens16),
+                            engine._ptr(tile_off), n, engine._ptr(pseudo), N_FLOWS, None, 0, engine._ptr(out),
+                            engine.current_stream())
+                return out
+        elif w.ragged and not name.endswith("d"):  # cfg4: the 16-byte packed layout (k_packed)
             arena, lens16, tile_chunk, lens = engine.gen_packed(n, 0, w.seed, w.hdr)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
-            run = lambda: engine.checksum_packed(arena, lens16, tile_chunk, n, pseudo, N_FLOWS)  # noqa: E731
+            out = torch.empty(n, dtype=torch.int16, device="cuda")
+
+            def run():  # the plain entry point: present in every build under A/B
+                engine.call("pipck_checksum_packed", engine._ptr(arena), engine._ptr(lens16), engine._ptr(tile_chunk),
+                            n, engine._ptr(pseudo), N_FLOWS, None, 0, engine._ptr(out), engine.current_stream())
+                return out
         elif w.ragged:  # cfg4d: 16-byte descriptors (pipck_checksum_ragged)
             arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
             nbytes = int(lens.to(torch.int64).sum().item()) + 2 * n
@@ -60,7 +75,8 @@ def worker(only: list[str], iters: int) -> None:
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
         ms = statistics.median(timed(run, iters) for _ in range(3))
         digest = hashlib.sha256(run().cpu().numpy().tobytes()).hexdigest()[:16]
-        tag = ("+pseudo" if fam and not w.family else "") + ("+desc" if name == "cfg4d" else "")
+        tag = ("+pseudo" if fam and not w.family else "") + ("+desc" if name == "cfg4d" else "") + \
+            ("+bytes" if name == "cfg4b" else "")
         print(json.dumps({"workload": w.name + tag, "packets": n, "ms": ms,
                           "bytes": nbytes, "sha": digest}), flush=True)
         del arena
