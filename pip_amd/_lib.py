@@ -54,7 +54,6 @@ SIGNATURES = {
     "pipck_verify_packed": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_packed_index": (_i32, [_p, _u64, _p, _p]),
     "pipck_checksum_packed_bytes": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
-    "pipck_tune_xcd_weights": (_i32, [_p, _u32]),
     "pipck_checksum_packed_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
     "pipck_verify_packed_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
     "pipck_checksum_packed_bytes_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
@@ -103,6 +102,7 @@ SIGNATURES = {
 INTERNAL_SIGNATURES = {
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
     "pipck_trace_tasks": (_i32, [_p, _u64]),
+    "pipck_tune_xcd_weights": (_i32, [_p, _u32]),
     "pipck_last_launch": (_i32, [C.c_char_p, _sz]),
 }
 
