@@ -173,9 +173,10 @@ def test_rx_verify_accepts_what_pip_emits_and_rejects_corruption():
     for p in pkts:
         v4 = p[0] >> 4 == 4
         hl = (p[0] & 15) * 4 if v4 else 40
-        # a byte of the IPv4 header that only its own checksum covers (TOS, id, fragment,
-        # TTL, the checksum itself), or a byte of the TCP/UDP segment
-        i = rng.choice([1, 4, 5, 6, 7, 8, 10, 11] if v4 and rng.random() < 0.5 else list(range(hl, len(p))))
+        # a byte of the IPv4 header that only its own checksum covers (TOS, id, TTL, the
+        # checksum itself; not the fragment field, which would make it a fragment whose
+        # payload is left unchecked), or a byte of the TCP/UDP segment
+        i = rng.choice([1, 4, 5, 8, 10, 11] if v4 and rng.random() < 0.5 else list(range(hl, len(p))))
         q = bytearray(p)
         q[i] ^= 0x10
         bad.append(bytes(q))
