@@ -2,7 +2,7 @@
 # Round-4 GPU session on one box: GPU tests, then the VERDICT r03 measurement
 # arms (XCD-weighted deal on cfg2, k_hdr result stream at 256M headers with
 # PMC passes) and a same-box A/B of this build against round 3's library.
-# STEPS picks a subset (tests xw hdr box bench ab); the first failure stops.
+# STEPS picks a subset (boxid tests xw hdr box bench ab); the first failure stops.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -12,6 +12,9 @@ mkdir -p "$OUT"
 for step in ${STEPS:-tests xw hdr ab}; do
   echo "== $step $(date +%T)"
   case $step in
+    boxid) # which machine / GPU this is (fresh boxes per call: compare sessions)
+           { echo "boot_id $(cat /proc/sys/kernel/random/boot_id)"; timeout 60 rocm-smi --showuniqueid --showserial --showbus 2>&1 | grep -E "GPU|0x|Serial|Unique|PCI" | head -8; } \
+             > "$OUT/boxid.txt" 2>&1; cat "$OUT/boxid.txt" ;;
     tests) timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
              > "$OUT/pytest.log" 2>&1 || { echo "pytest rc=$?"; tail -40 "$OUT/pytest.log"; exit 1; }
            tail -2 "$OUT/pytest.log" ;;
