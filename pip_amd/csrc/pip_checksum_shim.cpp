@@ -273,30 +273,33 @@ uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
 
 // The upper-layer header of an IPv6 packet: walks the extension headers whose
 // presence does not change the pseudo-header (hop-by-hop 0, destination
-// options 60, an atomic fragment 44).  Returns false when the payload's
-// checksum cannot be checked from this packet alone -- a real fragment (offset
-// or M flag set), a routing header 43 (the pseudo-header takes the FINAL
-// destination), or a chain too long or running past the payload.
-bool ipv6_upper(const uint8_t* b, uint32_t plen, uint8_t* proto, uint32_t* off) {
+// options 60, an atomic fragment 44).  Returns 1 with *proto / *off set; 0 when
+// the payload's checksum cannot be checked from this packet alone -- a real
+// fragment (offset or M flag set), a routing header 43 (the pseudo-header takes
+// the FINAL destination), more than 8 extension headers; -1 when a header runs
+// past the payload (malformed).
+int ipv6_upper(const uint8_t* b, uint32_t plen, uint8_t* proto, uint32_t* off) {
+    const uint32_t end = 40 + plen;
     uint8_t nh = b[6];
     uint32_t at = 40;
     for (int k = 0; k < 8; k++) {
         if (nh != 0 && nh != 60 && nh != 44) {
             *proto = nh;
             *off = at;
-            return nh != 43;
+            return nh == 43 ? 0 : 1;
         }
-        if (at + 8 > 40 + plen) return false;
+        if (at + 8 > end) return -1;
         const uint8_t* e = b + at;
         if (nh == 44) {
-            if (rd16(e + 2) & 0xFFF9u) return false;  // fragment offset (bits 15-3) or M (bit 0) set
+            if (rd16(e + 2) & 0xFFF9u) return 0;  // fragment offset (bits 15-3) or M (bit 0) set
             at += 8;
         } else {
             at += 8u * (e[1] + 1u);
         }
+        if (at > end) return -1;
         nh = e[0];
     }
-    return false;
+    return 0;
 }
 
 }  // namespace
@@ -333,7 +336,9 @@ uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t
             if (40 + plen > len) continue;
             ok[i] |= PIP_RX_IP_OK;  // IPv6 has no header checksum
             uint32_t off = 40;
-            if (!ipv6_upper(b, plen, &proto, &off)) {
+            const int up = ipv6_upper(b, plen, &proto, &off);
+            if (up < 0) continue;  // an extension header past the payload: L4 bits stay clear
+            if (up == 0) {
                 ok[i] |= PIP_RX_L4_OK;  // not checkable from this packet (fragment, routing header)
                 continue;
             }

@@ -335,6 +335,10 @@ def test_rx_verify_fragments_extension_headers_and_other_protocols(oracle):
         q[at + {6: 16, 17: 6, 58: 2}[nh]] ^= 0x40
         bad.append(bytes(q))
     assert (_verify(bad) == IP_OK | L4_CHECKED).all()
+    # an extension header whose length runs past the payload: malformed, no L4 bits
+    p = bytearray(_rx_packet(oracle, rng, 6, 6, 40, 1, ext=_ext([(0, 0)], 6)))
+    p[41] = 30  # hop-by-hop Hdr Ext Len: 248 bytes, past the 48-byte payload
+    assert list(_verify([bytes(p)])) == [IP_OK]
     # truncated ICMP (under 8 bytes) and TCP headers: no L4 bits
     short = [_rx_packet(oracle, rng, 4, 1, 4, 1), _rx_packet(oracle, rng, 6, 58, 6, 1), _rx_packet(oracle, rng, 4, 6, 12, 1)]
     assert list(_verify(short)) == [IP_OK, IP_OK, IP_OK]
