@@ -325,7 +325,8 @@ def run_rank(args) -> int:
             line["roofline"]["frac_rocprof"] = round(algo_bytes / (rocprof_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
 
     if env.rank == 0 and env.world == 1 and not args.no_cpu:
-        line["cpu_baseline"], line["host_end_to_end"] = cpu_legs(args, w, out, count, first)
+        dev = (arena, lens16, tile_off) if w.ragged else None
+        line["cpu_baseline"], line["host_end_to_end"] = cpu_legs(args, w, out, count, first, dev)
 
     shard.barrier(env)
     if env.rank == 0:
@@ -371,11 +372,48 @@ def chain_leg(ref, w, arena, offs, lens, flows, first, threads, want):
             "mpkt_per_s": round(len(lens) * reps / el / 1e6, 2), "results_match_flat": ok}
 
 
-def cpu_legs(args, w, gpu_out, count, first):
+def host_e2e_packed(w, dev, n, flows, want):
+    """PCIe-inclusive rate of the first n packets of a byte-packed ragged batch:
+    pinned host bytes + lengths -> pipck_host_checksum_packed_bytes (chunks H2D,
+    index, k_packedb, D2H) -> host results, checked against the GPU's."""
+    import ctypes as C
+
+    import torch
+
+    from pip_amd import _lib
+
+    arena, lens16, tile_off = dev
+    del tile_off
+    nb = int((lens16[:n].to(torch.int32) & 0xFFFF).sum().item())  # lengths are u16 stored as int16
+    h = torch.empty(max(nb, 1), dtype=torch.uint8, pin_memory=True)
+    h[:nb].copy_(arena[:nb])
+    hl = lens16[:n].cpu().numpy().view(np.uint16).copy()
+    out = np.zeros(n, dtype=np.uint16)
+    lib = _lib.load()
+    ctx = C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    fl = C.create_string_buffer(flows, max(len(flows), 1))
+    try:
+        call = lambda: lib.pipck_host_checksum_packed_bytes(  # noqa: E731
+            ctx, C.c_void_p(h.data_ptr()), C.c_void_p(hl.ctypes.data), n, w.family, fl, N_FLOWS, 0,
+            C.c_void_p(out.ctypes.data))
+        _lib.check("pipck_host_checksum_packed_bytes", call())
+        t0 = time.perf_counter()
+        for _ in range(3):
+            call()
+        e2e = nb * 3 / (time.perf_counter() - t0) / 2**30
+    finally:
+        lib.pipck_ctx_destroy(ctx)
+    return {"value": round(e2e, 2), "unit": "GiB/s", "sample_packets": n, "bytes": nb, "pinned": True,
+            "call": "pipck_host_checksum_packed_bytes (byte-packed, ~64 MiB chunks, two streams)",
+            "results_match": bool(np.array_equal(out, want))}
+
+
+def cpu_legs(args, w, gpu_out, count, first, dev=None):
     """pip's own checksum on the host cores over a bounded sample of the same
-    packets (checked bit-exact against the GPU results), plus -- for fixed
-    strides -- the PCIe-inclusive host -> device -> host rate of the same sample
-    through pipck_host_checksum_fixed."""
+    packets (checked bit-exact against the GPU results), plus the PCIe-inclusive
+    host -> device -> host rate of the same sample: pipck_host_checksum_fixed
+    for fixed strides, pipck_host_checksum_packed_bytes for the ragged batch."""
     import ctypes as C
 
     from oracle.oracle import Oracle, Reference
@@ -410,7 +448,9 @@ def cpu_legs(args, w, gpu_out, count, first):
                          f"1 thread: {st:.3f} GiB/s",
                "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified,
                "chain": chain_leg(ref, w, arena, offs, lens, flows, first, threads, res)}
-        return cpu, {"value": None, "note": "host end-to-end is measured for fixed strides (pipck_host_checksum_fixed)"}
+        e2e = host_e2e_packed(w, dev, n, flows, gpu[:n]) if dev is not None and first == 0 else \
+            {"value": None, "note": "host end-to-end: rank 0 of a one-rank run only"}
+        return cpu, e2e
 
     # fixed strides: cfg1's whole 1M-header batch is a 20 MB sample; others ~2 GiB
     n = args.cpu_sample or min(count, max(1, (2 << 30) // w.stride))

@@ -262,6 +262,16 @@ int pipck_host_sum(pipck_ctx* ctx, const pipck_hseg* segs, uint32_t nseg, uint32
 int pipck_host_checksum_fixed(pipck_ctx* ctx, const void* h_arena, uint64_t stride, uint32_t len,
                               uint64_t n_packets, int family, const void* h_flows, uint32_t n_flows,
                               uint64_t flow_origin, uint16_t* h_out);
+/* Host-resident byte-packed ragged batch (a capture buffer or a socket ring read
+ * in order: packet i's h_lens[i] bytes right after packet i-1's, no padding),
+ * the layout of pipck_checksum_packed_bytes: chunks of whole packets (~64 MiB)
+ * go H2D with their lengths, are indexed and checksummed on the device, and the
+ * results come back, double-buffered over two streams.  Flows, family and
+ * results as pipck_host_checksum_fixed (h_out[i] = pip_inet{,6}_checksum /
+ * pip_ip_checksum of packet i, host order).  Synchronous. */
+int pipck_host_checksum_packed_bytes(pipck_ctx* ctx, const void* h_arena, const uint16_t* h_lens, uint64_t n_packets,
+                                     int family, const void* h_flows, uint32_t n_flows, uint64_t flow_origin,
+                                     uint16_t* h_out);
 /* This context's per-packet path (pipck_host_sum): 0 = staged (H2D copy,
  * kernel, D2H copy), 1 = zero-copy (the kernel reads the pinned, coherent
  * staging buffer and writes the result to pinned host memory), 2 = auto

@@ -54,6 +54,7 @@ SIGNATURES = {
     "pipck_verify_packed": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
     "pipck_packed_index": (_i32, [_p, _u64, _p, _p]),
     "pipck_checksum_packed_bytes": (_i32, [_p, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p]),
+    "pipck_host_checksum_packed_bytes": (_i32, [_p, _p, _p, _u64, _i32, _p, _u32, _u64, _p]),
     "pipck_checksum_packed_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
     "pipck_verify_packed_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
     "pipck_checksum_packed_bytes_n": (_i32, [_p, _u64, _p, _p, _u64, _p, _u32, _p, _u64, _p, _p, _p]),

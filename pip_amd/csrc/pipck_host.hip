@@ -381,6 +381,12 @@ struct pipck_ctx {
     uint8_t* d_chunk[2] = {nullptr, nullptr};
     uint16_t* d_out[2] = {nullptr, nullptr};
     size_t chunk_cap = 0;
+    // byte-packed host batches (pipck_host_checksum_packed_bytes): per-chunk
+    // lengths and tile index, beside d_chunk / d_out
+    uint16_t* d_lens[2] = {nullptr, nullptr};
+    uint64_t* d_tile_off[2] = {nullptr, nullptr};
+    uint64_t packed_cap = 0;  // packets per chunk d_lens / d_tile_off hold
+    uint64_t out_cap = 0;     // results per chunk d_out holds
     uint32_t* d_pseudo = nullptr;
     void* d_flows = nullptr;
     uint32_t flows_cap = 0;
@@ -407,6 +413,56 @@ struct DeviceGuard {
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
+
+// The host pipelines' double-buffered device chunks: d_chunk[i] of at least
+// `bytes`, d_out[i] of at least `results` u16 (each grown on its own).
+int reserve_chunks(pipck_ctx* c, size_t bytes, uint64_t results) {
+    if (bytes > c->chunk_cap) {
+        for (int i = 0; i < 2; i++) {
+            if (c->d_chunk[i]) PIPCK_HIP(hipFree(c->d_chunk[i]));
+            c->d_chunk[i] = nullptr;
+        }
+        c->chunk_cap = 0;
+        for (int i = 0; i < 2; i++) PIPCK_HIP(hipMalloc((void**)&c->d_chunk[i], bytes));
+        c->chunk_cap = bytes;
+    }
+    if (results > c->out_cap) {
+        for (int i = 0; i < 2; i++) {
+            if (c->d_out[i]) PIPCK_HIP(hipFree(c->d_out[i]));
+            c->d_out[i] = nullptr;
+        }
+        c->out_cap = 0;
+        for (int i = 0; i < 2; i++) PIPCK_HIP(hipMalloc((void**)&c->d_out[i], results * sizeof(uint16_t)));
+        c->out_cap = results;
+    }
+    return PIPCK_OK;
+}
+
+// A host flow table to the device and its pseudo-header bases (stream 0; stream
+// 1 waits for them).  family 0: none, *d_pseudo = null.
+int upload_flows(pipck_ctx* c, int family, const void* h_flows, uint32_t n_flows, const uint32_t** d_pseudo) {
+    *d_pseudo = nullptr;
+    if (!family) return PIPCK_OK;
+    const size_t fbytes = (size_t)n_flows * (family == 4 ? sizeof(pipck_flow4) : sizeof(pipck_flow6));
+    if (n_flows > c->flows_cap) {
+        if (c->d_flows) PIPCK_HIP(hipFree(c->d_flows));
+        if (c->d_pseudo) PIPCK_HIP(hipFree(c->d_pseudo));
+        c->d_flows = nullptr;
+        c->d_pseudo = nullptr;
+        c->flows_cap = 0;
+        PIPCK_HIP(hipMalloc(&c->d_flows, (size_t)n_flows * sizeof(pipck_flow6)));
+        PIPCK_HIP(hipMalloc((void**)&c->d_pseudo, (size_t)n_flows * sizeof(uint32_t)));
+        c->flows_cap = n_flows;
+    }
+    PIPCK_HIP(hipMemcpyAsync(c->d_flows, h_flows, fbytes, hipMemcpyHostToDevice, c->stream[0]));
+    int rc = family == 4 ? pipck_flows4_prepare((const pipck_flow4*)c->d_flows, n_flows, c->d_pseudo, c->stream[0])
+                         : pipck_flows6_prepare((const pipck_flow6*)c->d_flows, n_flows, c->d_pseudo, c->stream[0]);
+    if (rc) return rc;
+    PIPCK_HIP(hipEventRecord(c->done[0], c->stream[0]));
+    PIPCK_HIP(hipStreamWaitEvent(c->stream[1], c->done[0], 0));
+    *d_pseudo = c->d_pseudo;
+    return PIPCK_OK;
+}
 
 // Modes 3 and 4: make sure the resident block runs (launching it if it never
 // ran or has exited after its idle timeout).
@@ -523,6 +579,8 @@ int pipck_ctx_destroy(pipck_ctx* c) {
         if (c->stream[i]) (void)hipStreamSynchronize(c->stream[i]);
         if (c->d_chunk[i]) (void)hipFree(c->d_chunk[i]);
         if (c->d_out[i]) (void)hipFree(c->d_out[i]);
+        if (c->d_lens[i]) (void)hipFree(c->d_lens[i]);
+        if (c->d_tile_off[i]) (void)hipFree(c->d_tile_off[i]);
         if (c->done[i]) (void)hipEventDestroy(c->done[i]);
         if (c->stream[i]) (void)hipStreamDestroy(c->stream[i]);
     }
@@ -707,6 +765,62 @@ int pipck_host_free(void* p) {
     return PIPCK_OK;
 }
 
+int pipck_host_checksum_packed_bytes(pipck_ctx* c, const void* h_arena, const uint16_t* h_lens, uint64_t n,
+                                     int family, const void* h_flows, uint32_t n_flows, uint64_t flow_origin,
+                                     uint16_t* h_out) {
+    if (!c || (n && (!h_arena || !h_lens || !h_out)) || (family != 0 && family != 4 && family != 6) ||
+        (family && (!h_flows || !n_flows))) {
+        set_error("pipck_host_checksum_packed_bytes: bad argument");
+        return PIPCK_EINVAL;
+    }
+    if (!n) return PIPCK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    const uint32_t* d_pseudo = nullptr;
+    int rc = upload_flows(c, family, h_flows, n_flows, &d_pseudo);
+    if (rc) return rc;
+    // Chunks of whole packets, ~64 MiB of bytes (at most kMaxPkts packets) each,
+    // double-buffered over the context's two streams: H2D of the chunk's bytes
+    // and lengths, its tile index (pipck_packed_bytes_index), k_packedb bounded
+    // by the chunk buffer, D2H of the results.
+    constexpr uint64_t kTarget = 64ull << 20, kMaxPkts = 1ull << 20;
+    if ((rc = reserve_chunks(c, (size_t)(kTarget + 65536 + 256), kMaxPkts))) return rc;  // overshoot < one packet
+    if (kMaxPkts > c->packed_cap) {
+        for (int i = 0; i < 2; i++) {
+            if (c->d_lens[i]) PIPCK_HIP(hipFree(c->d_lens[i]));
+            if (c->d_tile_off[i]) PIPCK_HIP(hipFree(c->d_tile_off[i]));
+            c->d_lens[i] = nullptr;
+            c->d_tile_off[i] = nullptr;
+        }
+        c->packed_cap = 0;
+        for (int i = 0; i < 2; i++) {
+            PIPCK_HIP(hipMalloc((void**)&c->d_lens[i], kMaxPkts * sizeof(uint16_t)));
+            PIPCK_HIP(hipMalloc((void**)&c->d_tile_off[i], (kMaxPkts / 64 + 2) * sizeof(uint64_t)));
+        }
+        c->packed_cap = kMaxPkts;
+    }
+    const uint8_t* src = (const uint8_t*)h_arena;
+    uint64_t first = 0, off = 0;
+    for (uint64_t k = 0; first < n; k++) {
+        uint64_t m = 0, bytes = 0;
+        while (first + m < n && m < kMaxPkts && bytes < kTarget) bytes += h_lens[first + m++];
+        const int b = (int)(k & 1);
+        hipStream_t s = c->stream[b];
+        if (bytes) PIPCK_HIP(hipMemcpyAsync(c->d_chunk[b], src + off, (size_t)bytes, hipMemcpyHostToDevice, s));
+        PIPCK_HIP(hipMemcpyAsync(c->d_lens[b], h_lens + first, m * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+        if ((rc = pipck_packed_bytes_index(c->d_lens[b], m, c->d_tile_off[b], s))) return rc;
+        rc = pipck_checksum_packed_bytes_n(c->d_chunk[b], c->chunk_cap, c->d_lens[b], c->d_tile_off[b], m, d_pseudo,
+                                           n_flows, nullptr, flow_origin + first, c->d_out[b], nullptr, s);
+        if (rc) return rc;
+        PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
+        first += m;
+        off += bytes;
+    }
+    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
+    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
+    return PIPCK_OK;
+}
+
 int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride, uint32_t len, uint64_t n,
                               int family, const void* h_flows, uint32_t n_flows, uint64_t flow_origin,
                               uint16_t* h_out) {
@@ -723,43 +837,12 @@ int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride
     std::lock_guard<std::mutex> lk(c->mu);
     DeviceGuard g(c->device);
     const uint32_t* d_pseudo = nullptr;
-    if (family) {
-        const size_t fbytes = (size_t)n_flows * (family == 4 ? sizeof(pipck_flow4) : sizeof(pipck_flow6));
-        if (n_flows > c->flows_cap) {
-            if (c->d_flows) PIPCK_HIP(hipFree(c->d_flows));
-            if (c->d_pseudo) PIPCK_HIP(hipFree(c->d_pseudo));
-            c->d_flows = nullptr;
-            c->d_pseudo = nullptr;
-            c->flows_cap = 0;
-            PIPCK_HIP(hipMalloc(&c->d_flows, (size_t)n_flows * sizeof(pipck_flow6)));
-            PIPCK_HIP(hipMalloc((void**)&c->d_pseudo, (size_t)n_flows * sizeof(uint32_t)));
-            c->flows_cap = n_flows;
-        }
-        PIPCK_HIP(hipMemcpyAsync(c->d_flows, h_flows, fbytes, hipMemcpyHostToDevice, c->stream[0]));
-        int rc = family == 4 ? pipck_flows4_prepare((const pipck_flow4*)c->d_flows, n_flows, c->d_pseudo, c->stream[0])
-                             : pipck_flows6_prepare((const pipck_flow6*)c->d_flows, n_flows, c->d_pseudo, c->stream[0]);
-        if (rc) return rc;
-        PIPCK_HIP(hipEventRecord(c->done[0], c->stream[0]));
-        PIPCK_HIP(hipStreamWaitEvent(c->stream[1], c->done[0], 0));
-        d_pseudo = c->d_pseudo;
-    }
+    int rc = upload_flows(c, family, h_flows, n_flows, &d_pseudo);
+    if (rc) return rc;
     // ~64 MiB chunks, double-buffered: chunk k uses stream k%2 (H2D -> kernel -> D2H)
     const uint64_t per_chunk = std::max<uint64_t>(1, (64ull << 20) / stride);
     const size_t chunk_bytes = (size_t)(per_chunk * stride);
-    if (chunk_bytes > c->chunk_cap) {
-        for (int i = 0; i < 2; i++) {
-            if (c->d_chunk[i]) PIPCK_HIP(hipFree(c->d_chunk[i]));
-            if (c->d_out[i]) PIPCK_HIP(hipFree(c->d_out[i]));
-            c->d_chunk[i] = nullptr;
-            c->d_out[i] = nullptr;
-        }
-        c->chunk_cap = 0;
-        for (int i = 0; i < 2; i++) {
-            PIPCK_HIP(hipMalloc((void**)&c->d_chunk[i], chunk_bytes));
-            PIPCK_HIP(hipMalloc((void**)&c->d_out[i], per_chunk * sizeof(uint16_t)));
-        }
-        c->chunk_cap = chunk_bytes;
-    }
+    if ((rc = reserve_chunks(c, chunk_bytes, per_chunk))) return rc;
     for (uint64_t first = 0, k = 0; first < n; first += per_chunk, k++) {
         const uint64_t m = std::min<uint64_t>(per_chunk, n - first);
         const int b = (int)(k & 1);
@@ -767,8 +850,8 @@ int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride
         const size_t bytes = (size_t)((m - 1) * stride + len);
         PIPCK_HIP(hipMemcpyAsync(c->d_chunk[b], (const uint8_t*)h_arena + first * stride, bytes,
                                  hipMemcpyHostToDevice, s));
-        int rc = pipck_checksum_fixed(c->d_chunk[b], stride, len, m, d_pseudo, n_flows, nullptr, flow_origin + first,
-                                      c->d_out[b], s);
+        rc = pipck_checksum_fixed(c->d_chunk[b], stride, len, m, d_pseudo, n_flows, nullptr, flow_origin + first,
+                                  c->d_out[b], s);
         if (rc) return rc;
         PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
     }

@@ -173,8 +173,8 @@ def test_injected_start_skew_lowers_the_aggregate(tmp_path, capfd, world):
         got[skew] = json.loads(next(ln for ln in out.splitlines() if ln.startswith("AGG "))[4:])
     flat, skewed = got[0.0], got[0.06]
     want_skew = (world - 1) * 60
-    assert flat["start_skew_ms"] < 30 and flat["span_s"] < flat["max_rank_s"] + 0.03
-    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 40
+    assert flat["start_skew_ms"] < 50 and flat["span_s"] < flat["max_rank_s"] + 0.05
+    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 100
     assert skewed["span_s"] >= skewed["max_rank_s"] + (want_skew - 5) / 1e3
     assert skewed["rate"] < 0.75 * skewed["rate_max_rank"]
     assert skewed["rate"] == pytest.approx(world * 1e9 * 5 / skewed["span_s"])

@@ -993,6 +993,55 @@ def test_host_pipeline_vs_oracle(oracle, pinned):
         lib.pipck_ctx_destroy(ctx)
 
 
+@pytest.mark.parametrize("shape", ["zipf_pinned", "zipf_pageable", "tiny_many", "after_fixed"])
+def test_host_packed_bytes_pipeline_vs_oracle(oracle, shape):
+    """pipck_host_checksum_packed_bytes: a byte-packed ragged batch in host
+    memory (cfg4's shape, packets back to back) through ~64 MiB chunks of whole
+    packets on two streams -- more than one chunk by bytes (Zipf) and by packet
+    count (1.2M packets of 0-40 bytes) -- against the oracle; and after the
+    fixed-stride pipeline sized the same context's buffers for 20-byte packets."""
+    lib = _lib.load()
+    ctx = C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    pin = None
+    try:
+        w = CFG4
+        if shape == "tiny_many":
+            n = 1_200_000
+            rng = np.random.default_rng(3)
+            lens = rng.integers(0, 41, n).astype(np.uint32)
+            offs = np.zeros(n, dtype=np.uint64)
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+            arena = rng.integers(0, 256, int(lens.sum()) + 16, dtype=np.uint8)
+        else:
+            n = 150_000
+            arena, offs, lens = oracle.gen_packed_bytes_batch(w.seed, 0, n, w.hdr)
+        if shape == "after_fixed":
+            hdrs = oracle.gen_fixed_batch(CFG1.seed, 0, 4 << 20, 20, CFG1.hdr, 20, 8)
+            tmp = np.zeros(4 << 20, dtype=np.uint16)
+            _lib.check("pipck_host_checksum_fixed", lib.pipck_host_checksum_fixed(
+                ctx, C.c_void_p(hdrs.ctypes.data), 20, 20, 4 << 20, 0, None, 0, 0, C.c_void_p(tmp.ctypes.data)))
+            assert np.array_equal(tmp[:5000], oracle.batch_fixed(hdrs, 20, 20, 5000, 0, 0, 0, 1, 0))
+        flows = oracle.flows_table(4, w.seed, N_FLOWS, w.proto)
+        lens16 = lens.astype(np.uint16)
+        out = np.zeros(n, dtype=np.uint16)
+        if shape == "zipf_pinned":
+            pin = lib.pipck_host_alloc(arena.size)
+            C.memmove(pin, arena.ctypes.data, arena.size)
+            src = C.c_void_p(pin)
+        else:
+            src = C.c_void_p(arena.ctypes.data)
+        fl = C.create_string_buffer(flows, len(flows))
+        _lib.check("pipck_host_checksum_packed_bytes", lib.pipck_host_checksum_packed_bytes(
+            ctx, src, C.c_void_p(lens16.ctypes.data), n, 4, fl, N_FLOWS, 7, C.c_void_p(out.ctypes.data)))
+        want = oracle.batch_ragged(arena, offs, lens, 4, w.proto, w.seed, N_FLOWS, 7, 8)
+        assert np.array_equal(out, want), np.nonzero(out != want)[0][:5]
+    finally:
+        if pin:
+            lib.pipck_host_free(pin)
+        lib.pipck_ctx_destroy(ctx)
+
+
 # ----------------------------------------------------------------------------
 # 7. generator shard invariance
 # ----------------------------------------------------------------------------
