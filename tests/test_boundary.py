@@ -100,6 +100,28 @@ def test_pip_tx_path_at_volume_matches_pip(family, mss):
             assert run(amd_bin, "--conns", conns, *m) == want, (conns, m)
 
 
+def test_tx_bench_on_pips_own_build_reports_resend_ages():
+    """CPU: pip's own build (no drop-in, no GPU) through the same TX driver --
+    the JSON line carries the stall metrics the drop-in runs are judged by, and
+    a resend by pip's timer is only ever classed as a stall when the segment
+    had waited >= 1 s (pip_tcp_check.cpp:25-39; the race at :45-56 resends
+    younger ones, profiles/r04_pip_timer_race.jsonl)."""
+    import json
+
+    ref_bin = ROOT / "oracle" / "_ref" / "stack_tx_ref"
+    if not ref_bin.exists():
+        pytest.skip("oracle/_ref is built where /root/reference exists")
+    for family in (4, 6):
+        r = subprocess.run([str(ref_bin), "--family", str(family), "--mss", "1460", "--bytes", str(64 << 20),
+                            "--write", str(1 << 20), "--conns", "2"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["retransmits"] == 0 and d["max_unacked_ms"] < 500 and d["max_action"] in (
+            "write", "ack input", "syn -> syn-ack", "handshake ack", "flush")
+        assert d["stale_clock_resends"] >= 0 and (d["stale_clock_resends"] == 0) == (d["max_resend_age_ms"] == 0)
+        assert d["packets"] > (64 << 20) // 1460
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("family,length", [(6, 8952), (4, 8972), (4, 1472)])
 def test_pip_udp_tx_path_matches_pip(family, length):
