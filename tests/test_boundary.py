@@ -364,3 +364,52 @@ def test_rx_verify_fragments_extension_headers_and_other_protocols(oracle):
     # truncated ICMP (under 8 bytes) and TCP headers: no L4 bits
     short = [_rx_packet(oracle, rng, 4, 1, 4, 1), _rx_packet(oracle, rng, 6, 58, 6, 1), _rx_packet(oracle, rng, 4, 6, 12, 1)]
     assert list(_verify(short)) == [IP_OK, IP_OK, IP_OK]
+
+
+@pytest.mark.gpu
+def test_rx_verify_reads_pinned_packets_in_place(oracle):
+    """Packets that lie in pinned memory (a tun read ring from pipck_host_alloc)
+    are read in place by the RX queue (auto zero-copy): same verdicts as the
+    same packets on the heap, at odd alignments inside the ring, mixed with heap
+    packets in one call, and after the ring is freed nothing refers to it."""
+    import ctypes as C
+    import random
+
+    import numpy as np
+
+    from pip_amd import _lib
+
+    rng = random.Random(23)
+    pkts = []
+    for k in range(600):
+        fam = rng.choice([4, 6])
+        proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
+        p = bytearray(_rx_packet(oracle, rng, fam, proto, rng.randint(20, 1500), k + 1))
+        if k % 5 == 0:
+            p[-1] ^= 0x20  # damaged payload byte: its L4 checksum fails
+        pkts.append(bytes(p))
+    heap_ok = _verify(pkts)
+    lib = _lib.load()
+    size = sum(len(p) + 7 for p in pkts) + 64
+    base = lib.pipck_host_alloc(size)
+    assert base
+    try:
+        ptrs, off = [], 3  # odd start: packets at arbitrary alignments
+        for i, p in enumerate(pkts):
+            C.memmove(base + off, p, len(p))
+            ptrs.append(base + off)
+            off += len(p) + (i % 7)
+        fn = C.CDLL(str(_lib.LIBSHIM)).pip_checksum_amd_verify_packets
+        fn.restype = C.c_uint32
+        fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p]
+        heap = [C.create_string_buffer(p, len(p)) for p in pkts]
+        # every other packet from the pinned ring, the rest from the heap
+        mix = [C.c_void_p(ptrs[i]) if i % 2 == 0 else C.cast(heap[i], C.c_void_p) for i in range(len(pkts))]
+        arr = (C.c_void_p * len(pkts))(*mix)
+        lens = (C.c_uint32 * len(pkts))(*[len(p) for p in pkts])
+        ok = np.zeros(len(pkts), dtype=np.uint8)
+        good = fn(arr, lens, len(pkts), ok.ctypes.data)
+        assert np.array_equal(ok, heap_ok) and good == int((ok == VERIFIED).sum())
+        assert (ok == VERIFIED).sum() > 300 and (ok == IP_OK | L4_CHECKED).sum() >= 100  # damaged: checked, failed
+    finally:
+        assert lib.pipck_host_free(base) == 0  # nothing still holds the ring
