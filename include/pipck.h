@@ -114,7 +114,10 @@ int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_
  * 1/8 bytes of metadata per packet instead of a 16-byte pipck_desc.  Flow of
  * packet i: d_flow_of ? d_flow_of[i] : (flow_origin + i) % n_flows; d_pseudo ==
  * NULL = pip_ip_checksum semantics.  Results as pipck_checksum_ragged
- * (pip_inet{,6}_checksum, pip_checksum.cpp:42-87).  d_arena 16-byte aligned. */
+ * (pip_inet{,6}_checksum, pip_checksum.cpp:42-87).  d_arena 16-byte aligned;
+ * a tile's loads start at the 128-byte line holding its first byte, so for an
+ * arena that is not 128-byte aligned the bytes of its first line before
+ * d_arena are loaded (same line, same page) and discarded. */
 int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk,
                           uint64_t n_packets, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                           uint64_t flow_origin, uint16_t* d_out, void* stream);
