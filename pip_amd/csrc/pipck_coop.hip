@@ -171,7 +171,9 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
     if (blocks > 0x7FFFFFFFull) return PIPCK_EINVAL;
     const size_t lds = 64u * coop_pitch(K) * sizeof(uint32_t);
     const uint32_t nf = n_flows ? n_flows : 1u;
-    const uint32_t u = ring ? ring : (jumbo ? 32u : 24u);
+    // a ring of 32 rows at every stride (2 waves/SIMD): at 1,488-B strides
+    // 0.887-0.891 ms against 0.894-0.897 for 24 (profiles/r04_cfg2_coop_scan.jsonl)
+    const uint32_t u = ring ? ring : 32u;
     static const coop_fn kCoop[3][2] = {  // [ring 16 / 24 / 32][verify], non-temporal loads
         {k_flat_coop<16, false, true>, k_flat_coop<16, true, true>},
         {k_flat_coop<24, false, true>, k_flat_coop<24, true, true>},

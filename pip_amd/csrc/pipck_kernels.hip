@@ -356,9 +356,9 @@ constexpr uint32_t kNoTaskEnd = 1u << 22;
 // bit 23: k_flat's task end computes every result but stores none
 // (MEASUREMENT ONLY, no results)
 constexpr uint32_t kEndNoStore = 1u << 23;
-// bit 28 (same results): the other fixed-stride schedule -- k_flat for jumbo
-// strides (default: the block-cooperative k_flat_coop, pipck_coop.hip),
-// k_flat_coop for shorter ones (default: k_flat)
+// bit 28 (same results): the other fixed-stride schedule -- k_flat (one task
+// per wave) instead of the block-cooperative k_flat_coop (pipck_coop.hip),
+// the default for strides from 1 KiB to 64 KiB since round 4
 constexpr uint32_t kFlatAltSchedule = 1u << 28;
 // EXPERIMENTAL (same results): bit 30 = per-wave result stores (the r02 scheme) instead of one coalesced
 // store of the whole block's results by its last wave; bit 31 = wave tasks of
@@ -1610,12 +1610,17 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
         const uint32_t cpp = (uint32_t)(stride / 16);
-        // Jumbo strides (>= 4 KiB, cfg3 / cfg5) take the block-cooperative stream
-        // (a block's four waves on interleaved rows of one task): cfg5 +0.6 %
-        // at 8M packets and +1.7 % at 1M, cfg3 +0.9 % at 1M over k_flat, on
-        // one box, one process (profiles/r03_flat_coop_scan.jsonl); at 1,488-B
-        // strides the two are even within 0.5 %, so cfg2 keeps k_flat.
-        const bool coop = (cpp >= 256) != ((g_tune.flags.load() & kFlatAltSchedule) != 0);
+        // Every stride from 1 KiB to 64 KiB takes the block-cooperative stream
+        // (a block's four waves on interleaved rows of one task, pipck_coop.hip).
+        // Jumbo strides since round 3: cfg5 +0.6 % at 8M packets and +1.7 % at
+        // 1M, cfg3 +0.9 % at 1M over k_flat (profiles/r03_flat_coop_scan.jsonl).
+        // Shorter strides since round 4, with a ring of 32 rows: cfg2 -1.2 to
+        // -1.5 % in time at 4M and 8M packets over three rounds, and -2.4 % /
+        // -1.8 % / -1.5 % at 1,488 / 3,072 / 4,000-B strides, even at 1 / 2 KiB
+        // (profiles/r04_cfg2_coop_scan.jsonl, r04_stride_scan.jsonl; one box,
+        // one process, results equal).  k_flat stays as the other schedule
+        // (tune bit 28) and for strides past 64 KiB.
+        const bool coop = (g_tune.flags.load() & kFlatAltSchedule) == 0;
         if (coop && stride <= 65536 &&
             launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, d_ok,
                              as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load(),

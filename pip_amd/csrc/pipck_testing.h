@@ -46,10 +46,10 @@ extern "C" {
  * Bits 21-23 launch separate probe kernels (k_flat_probe, k_flat_coop_probe:
  * checksum mode, non-temporal loads, rings 24/32 for k_flat); the production
  * kernels have them compiled out and ignore them otherwise.
- * Bit 28 = the other fixed-stride schedule: k_flat for jumbo strides (default
- * there: the block-cooperative k_flat_coop), k_flat_coop for shorter ones
- * (default there: k_flat); for k_flat_coop, bits 8..15 are rows per wave and
- * loads_per_lane 17/25/33 its ring.  Bit 29 = result stores with the r02
+ * Bit 28 = the other fixed-stride schedule: k_flat (one task per wave)
+ * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
+ * strides from 1 KiB to 64 KiB; for k_flat_coop, bits 8..15 are rows per wave
+ * (default 48, jumbo 64) and loads_per_lane 17/25/33 its ring (default 32).  Bit 29 = result stores with the r02
  * write-back policy in k_flat / k_packed instead of write-through (sc1).
  * Bit 30 = the r02 schemes: per-wave result stores in k_flat (default: one
  * coalesced store per block), tile rows from the tile's first chunk in k_packed

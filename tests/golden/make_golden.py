@@ -173,19 +173,23 @@ def sha(a) -> str:
 # config's pseudo-header (pip_ip_checksum semantics over the whole segment), so
 # all-zero packets fold to pip's ~fold(0) = 0xFFFF (pip/pip_checksum.cpp:29-38)
 # through the jumbo and byte-packed bench kernels too.  Each spec names the batch
-# kernel it exercises (tests/test_gpu_parity.py checks pipck_last_launch).
+# kernel it exercises (tests/test_gpu_parity.py checks pipck_last_launch), and
+# fixed strides of 1 KiB and more also the other schedule ("alt": k_flat, tune
+# bit 28) on the same bytes.
 EDGES = {
-    "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat<24,"},
-    "edge_flat32_udp6": {"cfg": 3, "n": 48, "ck_every": 2, "ck_off": 6, "kernel": "k_flat_coop<32,"},
+    "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat_coop<32,",
+                         "alt": "k_flat<24,"},
+    "edge_flat32_udp6": {"cfg": 3, "n": 48, "ck_every": 2, "ck_off": 6, "kernel": "k_flat_coop<32,",
+                         "alt": "k_flat<32,"},
     "edge_small_ip20": {"cfg": 1, "n": 4096, "ck_every": 5, "ck_off": 10, "zero_every": 7, "kernel": "k_small<"},
     "edge_packed_tcp4": {"cfg": 4, "n": 4096, "ck_every": 2, "ck_off": 16, "zero_every": 0, "kernel": "k_packed<"},
     "edge_packedb_tcp4": {"cfg": 4, "n": 4096, "ck_every": 3, "ck_off": 16, "zero_every": 0, "layout": "bytes",
                           "kernel": "k_packedb<"},
     "edge_flat_len0_v4": {"cfg": 2, "n": 256, "stride": 1024, "length": 0, "proto": 0, "zero_flows_every": 4,
-                          "kernel": "k_flat<24,"},
+                          "kernel": "k_flat_coop<32,", "alt": "k_flat<24,"},
     # no pseudo-header, all-zero packets -> 0xFFFF, self-checksummed ones -> 0x0000
     "edge_coop_nopseudo_tcp4": {"cfg": 5, "n": 96, "family": 0, "proto": 0, "ck_every": 4, "ck_off": 16,
-                                "zero_every": 3, "kernel": "k_flat_coop<32,"},
+                                "zero_every": 3, "kernel": "k_flat_coop<32,", "alt": "k_flat<32,"},
     "edge_packedb_nopseudo": {"cfg": 4, "n": 2048, "family": 0, "proto": 0, "ck_every": 5, "ck_off": 16,
                               "zero_every": 3, "layout": "bytes", "kernel": "k_packedb<"},
 }
@@ -284,7 +288,8 @@ def edge_batch(orc, ref, name: str, spec: dict) -> dict:
     assert n_zero + n_ffff > 0, name
     return {"cfg": w.cfg, "n": n, "first": first, "seed": w.seed, "stride": stride, "length": length, "hdr": w.hdr,
             "family": fam, "proto": proto, "n_flows": N_FLOWS, "zero_flows": zero_flows, "patches": patches,
-            "kernel": spec["kernel"], "layout": spec.get("layout", "padded16" if w.ragged else "fixed"),
+            "kernel": spec["kernel"], "alt": spec.get("alt"),
+            "layout": spec.get("layout", "padded16" if w.ragged else "fixed"),
             "arena_sha256": sha(arena), "results_sha256": sha(out.astype("<u2")),
             "head": [int(x) for x in out[:16]], "n_zero": n_zero, "n_ffff": n_ffff}
 

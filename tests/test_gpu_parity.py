@@ -181,7 +181,7 @@ def last_kernel() -> str:
 
 
 # the kernel each config's bench launch runs: the fixture pins THAT kernel
-BENCH_KERNEL = {1: "k_small<", 2: "k_flat<24,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
+BENCH_KERNEL = {1: "k_small<", 2: "k_flat_coop<32,", 3: "k_flat_coop<32,", 4: "k_packedb<", 5: "k_flat_coop<32,"}
 
 
 @pytest.mark.parametrize("name", sorted(ALL))
@@ -209,6 +209,14 @@ def test_batch_kernel_reproduces_pips_results(batches, name):
         outs = {"fixed": engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS, None,
                                                b["first"])}
         kernel = last_kernel()
+        if w.stride >= 1024:  # the other schedule (k_flat) on the same batch
+            engine.tune(alt_flat_schedule=True)
+            try:
+                outs["k_flat"] = engine.checksum_fixed(arena, b["stride"], b["length"], b["n"], pseudo, N_FLOWS,
+                                                       None, b["first"])
+                assert "k_flat<" in last_kernel()
+            finally:
+                engine.tune()
         if w.cfg == 1:  # the header row kernel that batches of >= 8M headers take (k_hdr)
             engine.tune(loads_per_lane=32)
             try:
@@ -264,6 +272,14 @@ def test_edge_fixture_through_batch_kernel(batches, name):
         out = engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None, b["first"])
     assert b["kernel"] in last_kernel(), last_kernel()
     outs = [out]
+    if b.get("alt"):  # the other fixed-stride schedule (k_flat) on the same bytes
+        engine.tune(alt_flat_schedule=True)
+        try:
+            outs.append(engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None,
+                                              b["first"]))
+            assert b["alt"] in last_kernel(), last_kernel()
+        finally:
+            engine.tune()
     if b["kernel"] == "k_small<" and not fam:  # IPv4 headers: also through k_hdr (batches >= 8M headers)
         engine.tune(loads_per_lane=32)
         try:
@@ -356,9 +372,9 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
     try:
         for stride, length in cases:
             for blocks in (0, 1, 7, 9, 17):  # < 8 blocks: one group; 9/17: uneven XCD groups
-                # k_flat itself at every stride (jumbo strides default to k_flat_coop)
+                # k_flat itself at every stride (the default from 1 KiB to 64 KiB is k_flat_coop)
                 engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, xcd_groups=xcd,
-                            alt_flat_schedule=stride >= 4096)
+                            alt_flat_schedule=True)
                 n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
                 host = rng.integers(0, 256, n * stride, dtype=np.uint8)
                 if n > 2:
@@ -389,8 +405,8 @@ def test_flat_coop_kernel_vs_oracle(oracle, ring, rows):
              (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
     try:
         for stride, length in cases:
-            # the coop stream is the default for jumbo strides, the alternative below 4 KiB
-            engine.tune(0, ring, 0, alt_flat_schedule=stride < 4096, rows_per_task=rows)
+            # the coop stream is the default for every stride from 1 KiB to 64 KiB
+            engine.tune(0, ring, 0, rows_per_task=rows)
             n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 700))
             host = rng.integers(0, 256, n * stride, dtype=np.uint8)
             if n > 2:
@@ -1573,14 +1589,16 @@ def test_flat_xcd_weighted_deal_same_results(oracle, weights):
     for n in (4096 * 8 + 7, 200003, 1 << 20):
         arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
         engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
-        want = u16(engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS))
-        assert "k_flat<24," in last_kernel()
-        engine.tune_xcd_weights(weights, max(weights))
+        engine.tune(alt_flat_schedule=True)  # k_flat (cfg2's default is k_flat_coop since round 4)
         try:
+            want = u16(engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS))
+            assert "k_flat<24," in last_kernel()
+            engine.tune_xcd_weights(weights, max(weights))
             got = u16(engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS))
             assert "k_flat_xw<24," in last_kernel(), last_kernel()
         finally:
             engine.tune_xcd_weights(None, 0)
+            engine.tune()
         assert np.array_equal(got, want), np.nonzero(got != want)[0][:5]
         host = arena[:2000 * w.stride].cpu().numpy()
         assert np.array_equal(got[:2000], oracle.batch_fixed(host, w.stride, w.length, 2000, 4, w.proto, w.seed,

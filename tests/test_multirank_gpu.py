@@ -258,7 +258,7 @@ def test_bench_line_names_its_kernel_and_build():
     assert r.returncode == 0, r.stderr[-3000:]
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     rf = d["roofline"]
-    assert rf["kernel"].startswith("void pipck::k_flat<24, true, false, true, 4>(")
+    assert rf["kernel"].startswith("void pipck::k_flat_coop<32, false, true>(")
     from pip_amd import _lib
 
     assert rf["lib_sha256"] == hashlib.sha256(Path(_lib.LIBPIPCK).read_bytes()).hexdigest()

@@ -101,12 +101,13 @@ def test_edge_fixtures_cover_both_corners(batches):
     # 0xFFFF under a pseudo-header (total 0: empty segment, zero addresses, proto 0)
     assert any(b["family"] and b["n_ffff"] for b in edges)
     # and 0x0000 through every batch kernel family the bench runs
-    kernels = {b["kernel"] for b in edges if b["n_zero"]}
+    kernels = {b["kernel"] for b in edges if b["n_zero"]} | {b["alt"] for b in edges if b["n_zero"] and b.get("alt")}
     assert {"k_flat<24,", "k_flat_coop<32,", "k_small<", "k_packed<", "k_packedb<"} <= kernels
     # and 0xFFFF (pip's ~fold(0), pip_checksum.cpp:29-38) through the jumbo and
     # byte-packed bench kernels, from all-zero packets with no pseudo-header
-    ffff = {b["kernel"] for b in edges if b["n_ffff"] and not b["family"]}
-    assert {"k_flat_coop<32,", "k_packedb<", "k_small<"} <= ffff
+    ffff = {b["kernel"] for b in edges if b["n_ffff"] and not b["family"]} | \
+        {b["alt"] for b in edges if b["n_ffff"] and not b["family"] and b.get("alt")}
+    assert {"k_flat_coop<32,", "k_flat<32,", "k_packedb<", "k_small<"} <= ffff
 
 
 def test_zipf_shape(oracle):

@@ -11,7 +11,9 @@
    is meant to remove).
 3. Timed A/B in one process, arms interleaved round by round: the median of K
    per-launch HIP event pairs per arm and round; results checked equal.
-One JSON line per step; the summary line last.
+One JSON line per step; the summary line last.  k_flat is cfg2's
+other schedule since round 4 (the default is k_flat_coop), so both arms run
+with tune bit 28 (alt_flat_schedule) set.
 """
 from __future__ import annotations
 
@@ -38,15 +40,18 @@ def last_kernel() -> str:
     return buf.value.decode()
 
 
+BASE = {"alt_flat_schedule": True}  # k_flat (and k_flat_xw), not k_flat_coop
+
+
 def traced(run, cap):
     buf = torch.zeros(cap * 4, dtype=torch.int64, device="cuda")
-    engine.tune(trace=True)
+    engine.tune(**BASE, trace=True)
     engine.call("pipck_trace_tasks", engine._ptr(buf), cap)
     torch.cuda.synchronize()
     out = run()
     torch.cuda.synchronize()
     engine.call("pipck_trace_tasks", None, 0)
-    engine.tune()
+    engine.tune(**BASE)
     rec = buf.view(-1, 4).cpu().numpy().view(np.uint64)
     rec = rec[rec[:, 2] > 0]
     t0 = rec[:, 1].astype(np.int64)
@@ -79,6 +84,7 @@ def main():
     ap.add_argument("--period", type=int, default=64)
     a = ap.parse_args()
     engine.require_gpu()
+    engine.tune(**BASE)
     w, n = CFG2, a.packets
     pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)[1]
     arena = torch.empty(n * w.stride, dtype=torch.uint8, device="cuda")
