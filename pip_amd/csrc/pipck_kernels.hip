@@ -1618,9 +1618,11 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // -1.5 % in time at 4M and 8M packets over three rounds, and -2.4 % /
         // -1.8 % / -1.5 % at 1,488 / 3,072 / 4,000-B strides, even at 1 / 2 KiB
         // (profiles/r04_cfg2_coop_scan.jsonl, r04_stride_scan.jsonl; one box,
-        // one process, results equal).  k_flat stays as the other schedule
-        // (tune bit 28) and for strides past 64 KiB.
-        const bool coop = (g_tune.flags.load() & kFlatAltSchedule) == 0;
+        // one process, results equal).  At the 1 and 2 KiB strides k_flat
+        // measured even to 1.3 % faster on the final build
+        // (r04_schedule_ab.jsonl), so those two keep it.  The other schedule
+        // is tune bit 28; strides past 64 KiB always take k_flat.
+        const bool coop = (stride != 1024 && stride != 2048) != ((g_tune.flags.load() & kFlatAltSchedule) != 0);
         if (coop && stride <= 65536 &&
             launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, d_ok,
                              as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load(),

@@ -48,7 +48,8 @@ extern "C" {
  * kernels have them compiled out and ignore them otherwise.
  * Bit 28 = the other fixed-stride schedule: k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
- * strides from 1 KiB to 64 KiB; for k_flat_coop, bits 8..15 are rows per wave
+ * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
+ * for k_flat_coop, bits 8..15 are rows per wave
  * (default 48, jumbo 64) and loads_per_lane 17/25/33 its ring (default 32).  Bit 29 = result stores with the r02
  * write-back policy in k_flat / k_packed instead of write-through (sc1).
  * Bit 30 = the r02 schemes: per-wave result stores in k_flat (default: one

@@ -174,8 +174,8 @@ def sha(a) -> str:
 # all-zero packets fold to pip's ~fold(0) = 0xFFFF (pip/pip_checksum.cpp:29-38)
 # through the jumbo and byte-packed bench kernels too.  Each spec names the batch
 # kernel it exercises (tests/test_gpu_parity.py checks pipck_last_launch), and
-# fixed strides of 1 KiB and more also the other schedule ("alt": k_flat, tune
-# bit 28) on the same bytes.
+# fixed strides of 1 KiB and more also the other schedule ("alt", tune bit 28:
+# k_flat where k_flat_coop is the default, and the reverse) on the same bytes.
 EDGES = {
     "edge_flat24_tcp4": {"cfg": 2, "n": 192, "ck_every": 3, "ck_off": 16, "kernel": "k_flat_coop<32,",
                          "alt": "k_flat<24,"},
@@ -186,7 +186,7 @@ EDGES = {
     "edge_packedb_tcp4": {"cfg": 4, "n": 4096, "ck_every": 3, "ck_off": 16, "zero_every": 0, "layout": "bytes",
                           "kernel": "k_packedb<"},
     "edge_flat_len0_v4": {"cfg": 2, "n": 256, "stride": 1024, "length": 0, "proto": 0, "zero_flows_every": 4,
-                          "kernel": "k_flat_coop<32,", "alt": "k_flat<24,"},
+                          "kernel": "k_flat<24,", "alt": "k_flat_coop<32,"},
     # no pseudo-header, all-zero packets -> 0xFFFF, self-checksummed ones -> 0x0000
     "edge_coop_nopseudo_tcp4": {"cfg": 5, "n": 96, "family": 0, "proto": 0, "ck_every": 4, "ck_off": 16,
                                 "zero_every": 3, "kernel": "k_flat_coop<32,", "alt": "k_flat<32,"},

@@ -272,7 +272,7 @@ def test_edge_fixture_through_batch_kernel(batches, name):
         out = engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None, b["first"])
     assert b["kernel"] in last_kernel(), last_kernel()
     outs = [out]
-    if b.get("alt"):  # the other fixed-stride schedule (k_flat) on the same bytes
+    if b.get("alt"):  # the other fixed-stride schedule on the same bytes
         engine.tune(alt_flat_schedule=True)
         try:
             outs.append(engine.checksum_fixed(arena, b["stride"], b["length"], n, pseudo, b["n_flows"], None,
@@ -372,9 +372,10 @@ def test_flat_stream_kernel_vs_oracle(oracle, rows, nt, xcd):
     try:
         for stride, length in cases:
             for blocks in (0, 1, 7, 9, 17):  # < 8 blocks: one group; 9/17: uneven XCD groups
-                # k_flat itself at every stride (the default from 1 KiB to 64 KiB is k_flat_coop)
+                # k_flat itself at every stride (the default from 1 KiB to 64 KiB is k_flat_coop,
+                # except at exactly 1 and 2 KiB)
                 engine.tune(0, rows, blocks, plain_loads=not nt, nt_loads=nt, xcd_groups=xcd,
-                            alt_flat_schedule=True)
+                            alt_flat_schedule=stride not in (1024, 2048))
                 n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 400))
                 host = rng.integers(0, 256, n * stride, dtype=np.uint8)
                 if n > 2:
@@ -405,8 +406,8 @@ def test_flat_coop_kernel_vs_oracle(oracle, ring, rows):
              (3072, 2049), (8960, 8960), (8992, 8980), (9216, 8980), (65536, 65535)]
     try:
         for stride, length in cases:
-            # the coop stream is the default for every stride from 1 KiB to 64 KiB
-            engine.tune(0, ring, 0, rows_per_task=rows)
+            # the coop stream is the default from 1 KiB to 64 KiB, except at exactly 1 and 2 KiB
+            engine.tune(0, ring, 0, rows_per_task=rows, alt_flat_schedule=stride in (1024, 2048))
             n = int(rng.integers(1, 20)) if stride > 20000 else int(rng.integers(1, 700))
             host = rng.integers(0, 256, n * stride, dtype=np.uint8)
             if n > 2:
