@@ -90,6 +90,6 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
 // The header row stream (pipck_hdr.hip): 20/24-byte strides, no pseudo-header;
 // PIPCK_EINVAL when the shape does not fit (the caller then takes k_small).
 int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint16_t* d_out,
-               uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags);
+               uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags, bool coop = false);
 
 }  // namespace pipck

@@ -79,7 +79,12 @@ __device__ __forceinline__ void hdr_lane(int lane, uint32_t len, u32x4& mH, u32x
     mT = u32x4{t[0], t[1], t[2], t[3]};
 }
 
-template <int D, int U, bool VERIFY, bool NT>
+// COOP (round 4): the block's four waves share ONE task of 4 x rows rows and
+// read interleaved rows (wave w: rows w, w+4, ...), so the block streams one
+// contiguous window, as k_flat_coop does for large packets; rows carry no
+// state across rows here (48 whole headers each), so nothing else changes but
+// the row order, and the block stores its results together at the end.
+template <int D, int U, bool VERIFY, bool NT, bool COOP = false>
 __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, uint32_t len, uint64_t n,
                                              uint32_t rows, uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
                                              uint32_t kflags) {
@@ -87,13 +92,13 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
     extern __shared__ uint16_t s_res[];  // 4 waves x rows * PR results
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t task = (uint64_t)blockIdx.x * 4 + w;
-    const uint64_t per = (uint64_t)rows * PR;  // headers per task
+    const uint64_t task = COOP ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * 4 + w;
+    const uint64_t per = (uint64_t)rows * PR * (COOP ? 4u : 1u);  // headers per task
     const uint64_t p0 = task * per;
-    if (p0 >= n) return;  // wave-uniform
+    if (p0 >= n) return;  // wave-uniform (block-uniform for COOP)
     const uint32_t np = (uint32_t)min<uint64_t>(per, n - p0);
     const uint32_t nrows = (np + PR - 1) / PR;
-    uint16_t* res = s_res + w * rows * PR;
+    uint16_t* res = COOP ? s_res : s_res + w * rows * PR;
     // the task's bytes as a range-checked buffer, to the 16-byte boundary after its last header
     const uint64_t b0 = p0 * (4u * D);
     const buf_t tb = buf_rsrc(arena + b0, (uint32_t)(((uint64_t)np * (4u * D) + 15u) & ~15ull));
@@ -101,14 +106,19 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
     int fin;
     hdr_lane<D>(lane, len, mH, mT, fin);
     const uint32_t loff = (uint32_t)lane < C ? 16u * lane : 0x7FFFFFF0u;  // lanes >= C: out of range, no request
+    // this wave's j-th row: j (one task per wave) or w + 4j (COOP)
+    const uint32_t rstep = COOP ? 4u : 1u, rbase = COOP ? w : 0u;
+    const uint32_t my_rows = COOP ? (nrows > w ? (nrows - w + 3u) / 4u : 0u) : nrows;
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) v[u] = buf_load<NT>(tb, (uint32_t)lane < C ? 16u * C * u + loff : loff);
-    for (uint32_t r0 = 0; r0 < nrows; r0 += U) {
+    for (int u = 0; u < U; u++)
+        v[u] = buf_load<NT>(tb, (uint32_t)lane < C ? 16u * C * (rbase + rstep * u) + loff : loff);
+    for (uint32_t j0 = 0; j0 < my_rows; j0 += U) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t r = r0 + u;
-            if (r < nrows) {  // wave-uniform
+            const uint32_t j = j0 + u;
+            const uint32_t r = rbase + rstep * j;
+            if (j < my_rows) {  // wave-uniform
                 const u32x4 x = v[u];
                 const uint32_t H = dot4(x & mH, 0u), T = dot4(x & mT, 0u);
                 // T of the lane before (wave_shr:1; lane 0 gets 0 and finishes nothing)
@@ -120,13 +130,16 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
                 }
             }
             // the row U ahead (unconditional: past the task it reads zeros, no request)
-            v[u] = buf_load<NT>(tb, (uint32_t)lane < C ? 16u * C * (r + U) + loff : loff);
+            v[u] = buf_load<NT>(tb, (uint32_t)lane < C ? 16u * C * (r + rstep * U) + loff : loff);
         }
     }
-    wave_sync();
+    if (COOP)
+        __syncthreads();  // every wave's rows in res before the block stores them
+    else
+        wave_sync();
     if (!VERIFY && (kflags & kHdrInPlace)) {  // measurement: results into the headers' ip_sum
         const buf_t hb = buf_rsrc(arena + b0, (uint32_t)((uint64_t)np * (4u * D)));
-        for (uint32_t i = lane; i < np; i += 64) {
+        for (uint32_t i = COOP ? threadIdx.x : (uint32_t)lane; i < np; i += COOP ? 256u : 64u) {
             const uint32_t r = res[i];
             __builtin_amdgcn_raw_buffer_store_b16((uint16_t)((r >> 8) | (r << 8)), hb, (int)(i * 4u * D + 10u), 0, 0);
         }
@@ -144,7 +157,8 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
         (VERIFY ? (uintptr_t)(ok + p0) : (uintptr_t)(out + p0)) % 16 == 0) {
         done = rbytes & ~15u;
         const uint32_t per_piece = VERIFY ? 16u : 8u;  // results per 16 bytes
-        for (uint32_t o = 16u * lane; o < done; o += 1024u) {
+        const uint32_t me = COOP ? threadIdx.x : (uint32_t)lane, nthr = COOP ? 256u : 64u;
+        for (uint32_t o = 16u * me; o < done; o += 16u * nthr) {
             const uint16_t* r = res + (o / 16u) * per_piece;
             u32x4 x;
             if (VERIFY) {  // 16 one-byte flags
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(256) void k_hdr(const uint8_t* __restrict__ arena, 
         }
         done /= VERIFY ? 1u : 2u;  // results stored
     }
-    for (uint32_t i = done + lane; i < np; i += 64) {
+    for (uint32_t i = done + (COOP ? threadIdx.x : (uint32_t)lane); i < np; i += COOP ? 256u : 64u) {
         if (VERIFY)
             store_result8(rb, i, res[i]);
         else
@@ -181,7 +195,7 @@ typedef void (*hdr_fn)(const uint8_t*, uint32_t, uint64_t, uint32_t, uint16_t*, 
 // flight per wave (8 / 16 / 24 / 32, 0 = auto).  PIPCK_EINVAL when the shape does
 // not fit (the caller then takes k_small).
 int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint16_t* d_out,
-               uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags) {
+               uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags, bool coop) {
     if ((stride != 20 && stride != 24) || len > stride || (uintptr_t)d_arena % 16) return PIPCK_EINVAL;
     const uint32_t PR = stride == 20 ? HdrGeom<5>::PR : HdrGeom<6>::PR;
     // rows per wave task: 32 with a ring of 32 (the whole task in flight at
@@ -197,11 +211,16 @@ int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, 
     const size_t lds = 4u * per * sizeof(uint16_t);
     const uint32_t u = ring ? ring : 32u;
     const int ui = u >= 32 ? 3 : (u >= 24 ? 2 : (u >= 16 ? 1 : 0));
-#define PIPCK_HD(D, U) {{k_hdr<D, U, false, false>, k_hdr<D, U, false, true>}, {k_hdr<D, U, true, false>, k_hdr<D, U, true, true>}}
-    static const hdr_fn kHdr[2][4][2][2] = {{PIPCK_HD(5, 8), PIPCK_HD(5, 16), PIPCK_HD(5, 24), PIPCK_HD(5, 32)},
-                                            {PIPCK_HD(6, 8), PIPCK_HD(6, 16), PIPCK_HD(6, 24), PIPCK_HD(6, 32)}};  // [D][ring][verify][nt]
+#define PIPCK_HD(D, U, CO) {{k_hdr<D, U, false, false, CO>, k_hdr<D, U, false, true, CO>}, \
+                           {k_hdr<D, U, true, false, CO>, k_hdr<D, U, true, true, CO>}}
+    static const hdr_fn kHdr[2][2][4][2][2] = {  // [coop][D][ring][verify][nt]
+        {{PIPCK_HD(5, 8, false), PIPCK_HD(5, 16, false), PIPCK_HD(5, 24, false), PIPCK_HD(5, 32, false)},
+         {PIPCK_HD(6, 8, false), PIPCK_HD(6, 16, false), PIPCK_HD(6, 24, false), PIPCK_HD(6, 32, false)}},
+        {{PIPCK_HD(5, 8, true), PIPCK_HD(5, 16, true), PIPCK_HD(5, 24, true), PIPCK_HD(5, 32, true)},
+         {PIPCK_HD(6, 8, true), PIPCK_HD(6, 16, true), PIPCK_HD(6, 24, true), PIPCK_HD(6, 32, true)}}};
 #undef PIPCK_HD
-    PIPCK_LAUNCH(kHdr[stride == 24][ui][verify][nt], dim3((uint32_t)blocks), dim3(256), lds, s,
+    // a block covers 4 x R rows either way: four wave tasks, or one cooperative task
+    PIPCK_LAUNCH(kHdr[coop][stride == 24][ui][verify][nt], dim3((uint32_t)blocks), dim3(256), lds, s,
                  (const uint8_t*)d_arena, len, n, R, d_out, d_ok, kflags);
     PIPCK_LAUNCHED("k_hdr");
     return PIPCK_OK;

@@ -1695,11 +1695,14 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     // 1 = never k_hdr.
     {
         const uint32_t lq = g_tune.loads.load(), flags = g_tune.flags.load();
+        // loads_per_lane 8/16/24/32 = one task per wave with that ring, 9/17/25/33 =
+        // the block-cooperative row order with ring 8/16/24/32
         const bool force = lq == 8 || lq == 16 || lq == 24 || lq == 32;
+        const bool force_coop = lq == 9 || lq == 17 || lq == 25 || lq == 33;
         if (!d_pseudo && (stride == 20 || stride == 24) && !g_tune.lanes.load() && lq != 1 &&
-            (force || n >= kHdrMinBatch) &&
+            (force || force_coop || n >= kHdrMinBatch) &&
             launch_hdr(verify, d_arena, stride, len, n, d_out, d_ok, as_stream(stream), (flags >> 8) & 0xFFu,
-                       force ? lq : 0u, nt_for(true), flags) == PIPCK_OK)
+                       force ? lq : (force_coop ? lq - 1 : 0u), nt_for(true), flags, force_coop) == PIPCK_OK)
             return PIPCK_OK;
     }
     // Tiny 8-B-multiple strides with pseudo-headers (pure ACKs, small UDP) or

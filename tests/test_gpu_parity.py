@@ -538,19 +538,22 @@ def test_small_packet_kernel_vs_oracle(oracle, misalign):
 
 
 @pytest.mark.parametrize("stride", [20, 24])
-@pytest.mark.parametrize("ring,rows", [(32, 0), (8, 1), (16, 3), (24, 64), (16, 128)])
+@pytest.mark.parametrize("ring,rows", [(32, 0), (8, 1), (16, 3), (24, 64), (16, 128),
+                                       (33, 0), (9, 1), (17, 3), (25, 64), (17, 128)])
 def test_header_row_kernel_vs_oracle(oracle, stride, ring, rows):
     """k_hdr (pipck_hdr.hip): packed 20/24-byte items with no pseudo-header
     (cfg1's IPv4 headers) streamed as rows of whole headers, each header split
     over two lanes.  Every length up to the stride (bytes past `len` masked,
-    odd lengths), batches ending inside a row, on a row and on a task boundary,
-    all-0xFF / all-zero headers, RX verify; every ring and task size."""
+    odd lengths), batches ending inside a row, on a row, on a wave-task and on
+    a block-task boundary, all-0xFF / all-zero headers, RX verify; every ring
+    and task size, one task per wave (ring 8/16/24/32) and the block-cooperative
+    row order (9/17/25/33)."""
     rng = np.random.default_rng(700 + stride + ring + rows)
     engine.tune(0, ring, 0, rows_per_task=rows)
     try:
         per = (rows or 64) * (48 if stride == 20 else 42)  # headers per wave task
         for length in sorted({0, 1, 2, 3, 4, 5, 11, 19, 20, stride - 1, stride}):
-            for n in sorted({1, 47, 48, 49, per - 1, per, per + 1, 4 * per + 7, 20000}):
+            for n in sorted({1, 47, 48, 49, per - 1, per, per + 1, 4 * per - 1, 4 * per, 4 * per + 7, 20000}):
                 host = rng.integers(0, 256, n * stride + 16, dtype=np.uint8)
                 if n > 3:
                     host[stride:2 * stride] = 0xFF
