@@ -71,6 +71,9 @@ def parse(argv=None):
     p.add_argument("--traffic", default="auto",
                    help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json); "
                         "attached only if measured on this exact kernel of this exact libpipck.so build")
+    p.add_argument("--tune", default="",
+                   help="measurement only: JSON of engine.tune kwargs (internal launch-shape override); "
+                        "the line then names it in config.tune_override")
     p.add_argument("--start-skew-ms", type=float, default=0.0,
                    help="rehearsal/test only: rank r waits r x this after the barrier before its timed start")
     p.add_argument("--share-gpus", action="store_true",
@@ -158,6 +161,8 @@ def run_rank(args) -> int:
         return 3
     torch.cuda.set_device(dev)
     engine.require_gpu()
+    if args.tune:
+        engine.tune(**json.loads(args.tune))
     import socket
 
     placement = {"rank": env.rank, "host": socket.gethostname(), "device": dev, "pci_bus_id": engine.pci_bus_id(dev),
@@ -274,6 +279,7 @@ def run_rank(args) -> int:
             "arena_stride": w.stride,
             "layout": "byte-packed (no padding), u16 lengths + u64 byte offset per 64 packets" if w.ragged
                       else f"fixed {w.stride}-byte slots",
+            **({"tune_override": json.loads(args.tune)} if args.tune else {}),
             "parallelism": f"{env.world} shard(s), contiguous packet ranges"
                            f"{' of equal bytes' if w.ragged else ''}, no data-path collective"
                            f"{f', {env.world} ranks SHARING {env.world - n_shared} GPU(s) (--share-gpus)' if n_shared else ''}",

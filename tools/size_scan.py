@@ -25,6 +25,20 @@ DEFAULT_SIZES = {1: (1 << 20,), 2: (4 << 20,), 3: (1 << 20,), 4: (8 << 20, 32 <<
                  5: (2 << 20, 4 << 20, 8 << 20, 16 << 20)}
 
 
+def timed_b2b(fn, iters):
+    """bench.py's timing: iters launches back to back (no host sync between
+    them), an event pair around each, median per-dispatch time."""
+    fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    return statistics.median(a.elapsed_time(b) for a, b in ev)
+
+
 def timed(fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -48,7 +62,10 @@ def main():
     ap.add_argument("--packed", action="store_true", help="ragged workloads: the 16-B packed-lengths kernel")
     ap.add_argument("--packedb", action="store_true", help="ragged workloads: the byte-packed kernel (bench.py's)")
     ap.add_argument("--arms", default="", help="JSON {arm: engine.tune kwargs}, or @file (default: built-in arms)")
+    ap.add_argument("--b2b", action="store_true",
+                    help="time launches back to back as bench.py does (default: a host sync after every launch)")
     a = ap.parse_args()
+    clock = timed_b2b if a.b2b else timed
     engine.require_gpu()
     plan = [(CFG5, (2 << 20, 4 << 20, 8 << 20, 16 << 20)), (CFG4, (8 << 20, 32 << 20))]
     if a.only:
@@ -88,7 +105,7 @@ def main():
             for rnd in range(5):
                 for xcd, kw in arms.items():
                     engine.tune(**kw)
-                    res.setdefault(xcd, []).append(timed(run, a.iters))
+                    res.setdefault(xcd, []).append(clock(run, a.iters))
                     out = run()
                     if rnd == 0 and xcd == next(iter(arms)):
                         ref = out.clone()
@@ -97,7 +114,8 @@ def main():
             for xcd, ms in res.items():
                 m = statistics.median(ms)
                 print(json.dumps({"workload": w.name, "packets": n, "gbytes": round(nbytes / 1e9, 1), "bytes": nbytes,
-                                  "arm": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1)}),
+                                  "arm": xcd, "ms": round(m, 4), "GBps": round(nbytes / m / 1e6, 1),
+                                  "timing": "back to back" if a.b2b else "synced"}),
                       flush=True)
             engine.tune()
             del arena
