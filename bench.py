@@ -63,7 +63,10 @@ def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    # the GPU's clocks ramp for ~25 ms of work after an idle gap (profiles/
+    # r04_ramp.jsonl): 40 warmup launches cover it for every config (cfg2-4 run
+    # ~1 ms per launch; the driver's --warmup 5 already covers cfg5's 10 ms)
+    p.add_argument("--warmup", type=int, default=40)
     p.add_argument("--workload", default="cfg5", help="cfg1..cfg5 (default: the headline cfg5)")
     p.add_argument("--packets-per-gpu", type=int, default=0, help="override the per-GPU shard size")
     p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")

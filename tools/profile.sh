@@ -21,7 +21,7 @@ run() {  # $1 = name, rest = rocprofv3 args
   echo "   rc=$rc"; tail -2 "$OUT/$name.err"
   [ $rc -eq 0 ] || exit $rc
 }
-run trace --kernel-trace --stats  # bench defaults: 20 steps, 5 warmup
+run trace --kernel-trace --stats  # bench defaults: 20 steps, 40 warmup
 BENCH_ARGS="$BENCH_ARGS --steps 3 --warmup 1"
 run pmc_fetch --pmc FETCH_SIZE
 run pmc_write --pmc WRITE_SIZE
