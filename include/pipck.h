@@ -365,6 +365,38 @@ int pipck_txq_complete(pipck_txq* q);
 /* packets submitted and not yet completed */
 uint64_t pipck_txq_inflight(const pipck_txq* q);
 
+/* ---- RX verification of received packets --------
+ * pip never checks a received checksum (pip/pip_netif.cpp:45-77 hands packets
+ * to TCP / UDP / ICMP as they come).  pipck_rx_verify checks n IP packets as
+ * read from the tun device (IPv4 or IPv6, pkts[i] of lens[i] bytes, link
+ * padding after the IP length allowed) in one call and sets ok[i]:
+ *   PIPCK_RX_IP_OK       the IPv4 header checksum verifies (always set for IPv6)
+ *   PIPCK_RX_L4_OK       no payload checksum failed: it verified, or there was
+ *                        none this can check (PIPCK_RX_L4_CHECKED clear)
+ *   PIPCK_RX_L4_CHECKED  the payload's checksum was computed: TCP / UDP over
+ *                        their pseudo-headers (pip_inet{,6}_checksum), ICMPv4
+ *                        over the message (pip_ip_checksum, RFC 792), ICMPv6
+ *                        over the IPv6 pseudo-header, next header 58
+ * ok[i] == PIPCK_RX_VERIFIED (7): both checksums computed and verified; 3:
+ * nothing failed but the payload was NOT checked (an IPv4 or IPv6 fragment, an
+ * IPv6 routing header, UDP over IPv4 with a zero checksum, another protocol);
+ * malformed lengths or a truncated TCP/UDP/ICMP header leave the L4 bits
+ * clear; not IPv4/IPv6, 0.  IPv6 hop-by-hop / destination-options headers and
+ * atomic fragments are walked to the upper layer.  Packets that lie in pinned
+ * memory (pipck_host_alloc / pipck_host_register) are read in place by the GPU
+ * and their ranges held until the call returns; others are copied.  Returns
+ * when every ok[i] is set; *n_verified (optional) = packets with ok == 7.
+ * One queue per thread (not thread-safe). */
+#define PIPCK_RX_IP_OK 1u
+#define PIPCK_RX_L4_OK 2u
+#define PIPCK_RX_L4_CHECKED 4u
+#define PIPCK_RX_VERIFIED 7u
+typedef struct pipck_rxq pipck_rxq;
+int pipck_rxq_create(pipck_ctx* ctx, pipck_rxq** out);
+int pipck_rxq_destroy(pipck_rxq* q);
+int pipck_rx_verify(pipck_rxq* q, const void* const* pkts, const uint32_t* lens, uint64_t n, uint8_t* ok,
+                    uint64_t* n_verified);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,6 +97,9 @@ SIGNATURES = {
     "pipck_txq_inflight": (_u64, [_p]),
     "pipck_txq_auto_zero_copy": (_i32, [_p, _i32]),
     "pipck_txq_inplace_max": (_i32, [_p, _u64]),
+    "pipck_rxq_create": (_i32, [_p, C.POINTER(_p)]),
+    "pipck_rxq_destroy": (_i32, [_p]),
+    "pipck_rx_verify": (_i32, [_p, _p, _p, _u64, _p, C.POINTER(_u64)]),
 }
 
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only

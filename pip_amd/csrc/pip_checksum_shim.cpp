@@ -29,7 +29,7 @@ namespace {
 struct ThreadCtx {
     pipck_ctx* ctx = nullptr;
     pipck_txq* txq = nullptr;
-    pipck_txq* rxq = nullptr;  // pip_checksum_amd_verify_packets: received packets, never pip's TX batch
+    pipck_rxq* rxq = nullptr;  // pip_checksum_amd_verify_packets: received packets, never pip's TX batch
     bool zero_copy = false;  // pip_checksum_amd_zero_copy(): pinned segments read in place at flush
     bool capture = false;    // pip_checksum_amd_capture(): pip's TX calls queue instead of computing
     // Chains whose pinned segments a batch reads in place stay referenced until
@@ -37,7 +37,7 @@ struct ThreadCtx {
     // `keep` for the batch receiving adds, `keep_inflight` for the submitted one.
     std::vector<std::shared_ptr<pip_buf>> keep, keep_inflight;
     ~ThreadCtx() {
-        if (rxq) pipck_txq_destroy(rxq);
+        if (rxq) pipck_rxq_destroy(rxq);
         if (txq) pipck_txq_destroy(txq);  // waits for the in-flight batch
         keep.clear();
         keep_inflight.clear();
@@ -250,56 +250,18 @@ void pip_checksum_amd_capture(bool on) { t_ctx.capture = on; }
 // ---- RX batch verification ------------------------
 // pip never checks a received checksum (pip/pip_netif.cpp:45-77,
 // pip/protocol/pip_tcp_input.cpp, pip/protocol/pip_udp.cpp:11-26).  Received
-// packets go through a second per-thread queue (pip's TX queue is left alone):
-// each IPv4 header and each TCP / UDP segment is queued with its stored
-// checksum INCLUDED, so pip's arithmetic yields 0x0000 exactly for a packet
-// that verifies, and the queue stores that result into a scratch word.
+// packets go to this thread's RX queue (pipck_rx_verify, pip_amd/csrc/
+// pipck_rx.hip): the host parses what each checksum covers, one kernel per
+// chunk of packets sums and checks them, reading packets in pinned memory in
+// place.  pip's deferred TX batch is not touched.
 namespace {
 
-// this thread's RX queue (a member of the thread's context, so it is destroyed
-// before the HIP context it was created on)
-pipck_txq* rx_queue() {
+pipck_rxq* rx_queue() {
     if (!t_ctx.rxq) {
-        int rc = pipck_txq_create(t_ctx.get(), &t_ctx.rxq);
-        if (rc) die("pipck_txq_create", rc);
-        // packets already in pinned memory (a registered tun read ring) are read in place
-        rc = pipck_txq_auto_zero_copy(t_ctx.rxq, 1);
-        if (rc) die("pipck_txq_auto_zero_copy", rc);
+        int rc = pipck_rxq_create(t_ctx.get(), &t_ctx.rxq);
+        if (rc) die("pipck_rxq_create", rc);
     }
     return t_ctx.rxq;
-}
-
-uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
-
-// The upper-layer header of an IPv6 packet: walks the extension headers whose
-// presence does not change the pseudo-header (hop-by-hop 0, destination
-// options 60, an atomic fragment 44).  Returns 1 with *proto / *off set; 0 when
-// the payload's checksum cannot be checked from this packet alone -- a real
-// fragment (offset or M flag set), a routing header 43 (the pseudo-header takes
-// the FINAL destination), more than 8 extension headers; -1 when a header runs
-// past the payload (malformed).
-int ipv6_upper(const uint8_t* b, uint32_t plen, uint8_t* proto, uint32_t* off) {
-    const uint32_t end = 40 + plen;
-    uint8_t nh = b[6];
-    uint32_t at = 40;
-    for (int k = 0; k < 8; k++) {
-        if (nh != 0 && nh != 60 && nh != 44) {
-            *proto = nh;
-            *off = at;
-            return nh == 43 ? 0 : 1;
-        }
-        if (at + 8 > end) return -1;
-        const uint8_t* e = b + at;
-        if (nh == 44) {
-            if (rd16(e + 2) & 0xFFF9u) return 0;  // fragment offset (bits 15-3) or M (bit 0) set
-            at += 8;
-        } else {
-            at += 8u * (e[1] + 1u);
-        }
-        if (at > end) return -1;
-        nh = e[0];
-    }
-    return 0;
 }
 
 }  // namespace
@@ -307,80 +269,13 @@ int ipv6_upper(const uint8_t* b, uint32_t plen, uint8_t* proto, uint32_t* off) {
 uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n, uint8_t* ok) {
     if (!n) return 0;
     if (!pkts || !lens || !ok) die("pip_checksum_amd_verify_packets: null argument", PIPCK_EINVAL);
-    std::vector<uint16_t> ip_res(n, 0xFFFFu), l4_res(n, 0xFFFFu);  // htons(result) lands here; 0 = verified
-    std::vector<uint8_t> queued(n, 0);                              // bit 0: IP header queued, bit 1: L4 message
-    pipck_txq* q = rx_queue();
-    for (uint32_t i = 0; i < n; i++) {
-        ok[i] = 0;
-        const uint8_t* b = (const uint8_t*)pkts[i];
-        const uint32_t len = lens[i];
-        if (!b || len < 20) continue;
-        const uint8_t* l4 = nullptr;
-        uint32_t l4len = 0;
-        uint8_t proto = 0;
-        int rc = 0;
-        const bool v4 = (b[0] >> 4) == 4;
-        if (v4) {
-            const uint32_t ihl = (b[0] & 15u) * 4u, total = rd16(b + 2);
-            if (ihl < 20 || total < ihl || total > len) continue;  // malformed: 0
-            rc = pipck_txq_add_ip(q, b, ihl, &ip_res[i]);          // the header with its ip_sum
-            if (rc) die("pipck_txq_add_ip", rc);
-            queued[i] |= 1;
-            if (rd16(b + 6) & 0x3FFFu) {  // MF or a fragment offset: the L4 checksum spans the reassembled datagram
-                ok[i] |= PIP_RX_L4_OK;
-                continue;
-            }
-            proto = b[9], l4 = b + ihl, l4len = total - ihl;
-        } else if ((b[0] >> 4) == 6 && len >= 40) {
-            const uint32_t plen = rd16(b + 4);
-            if (40 + plen > len) continue;
-            ok[i] |= PIP_RX_IP_OK;  // IPv6 has no header checksum
-            uint32_t off = 40;
-            const int up = ipv6_upper(b, plen, &proto, &off);
-            if (up < 0) continue;  // an extension header past the payload: L4 bits stay clear
-            if (up == 0) {
-                ok[i] |= PIP_RX_L4_OK;  // not checkable from this packet (fragment, routing header)
-                continue;
-            }
-            l4 = b + off, l4len = 40 + plen - off;
-        } else {
-            continue;
-        }
-        const bool icmp = v4 ? proto == IPPROTO_ICMP : proto == IPPROTO_ICMPV6;
-        if (proto != IPPROTO_TCP && proto != IPPROTO_UDP && !icmp) {
-            ok[i] |= PIP_RX_L4_OK;  // a protocol without a checksum this helper knows: unchecked
-            continue;
-        }
-        if (l4len < (proto == IPPROTO_TCP ? 20u : 8u)) continue;  // truncated: L4 bits stay clear
-        if (proto == IPPROTO_UDP && v4 && !l4[6] && !l4[7]) {
-            ok[i] |= PIP_RX_L4_OK;  // UDP over IPv4 without a checksum (RFC 768): unchecked
-            continue;
-        }
-        const pipck_hseg seg{l4, l4len};
-        if (icmp && v4) {
-            // ICMPv4: pip_ip_checksum over the whole message, no pseudo-header (RFC 792)
-            rc = pipck_txq_add_ip(q, l4, l4len, &l4_res[i]);
-        } else if (v4) {
-            uint32_t src = 0, dst = 0;  // network order, as in struct in_addr
-            std::memcpy(&src, b + 12, 4);
-            std::memcpy(&dst, b + 16, 4);
-            rc = pipck_txq_add4(q, &seg, 1, proto, src, dst, &l4_res[i]);
-        } else {
-            // TCP, UDP and ICMPv6 (next header 58, RFC 4443 2.3) over the IPv6 pseudo-header
-            rc = pipck_txq_add6(q, &seg, 1, proto, b + 8, b + 24, &l4_res[i]);
-        }
-        if (rc) die("pipck_txq_add (rx)", rc);
-        queued[i] |= 2;
-    }
-    int rc = pipck_txq_flush(q);
-    if (rc) die("pipck_txq_flush", rc);
-    uint32_t good = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        if ((queued[i] & 1) && ip_res[i] == 0) ok[i] |= PIP_RX_IP_OK;
-        if (queued[i] & 2) ok[i] |= (l4_res[i] == 0 ? PIP_RX_L4_OK : 0) | PIP_RX_L4_CHECKED;
-        good += ok[i] == PIP_RX_VERIFIED;
-    }
-    return good;
+    static_assert(PIP_RX_IP_OK == PIPCK_RX_IP_OK && PIP_RX_L4_OK == PIPCK_RX_L4_OK &&
+                      PIP_RX_L4_CHECKED == PIPCK_RX_L4_CHECKED && PIP_RX_VERIFIED == PIPCK_RX_VERIFIED,
+                  "the drop-in's RX bits are pipck_rx_verify's");
+    uint64_t good = 0;
+    int rc = pipck_rx_verify(rx_queue(), pkts, lens, n, ok, &good);
+    if (rc) die("pipck_rx_verify", rc);
+    return (uint32_t)good;
 }
 
 bool pip_checksum_amd_capturing() { return t_ctx.capture; }

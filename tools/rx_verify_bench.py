@@ -49,6 +49,8 @@ def main():
                 pk[:, 0] = 0x45
                 pk[:, 2] = size >> 8
                 pk[:, 3] = size & 0xFF
+                pk[:, 6] = 0x40  # DF, offset 0: not a fragment (a fragment's L4 is not checked)
+                pk[:, 7] = 0
                 pk[:, 9] = 6
                 base = buf.ctypes.data
                 ptrs = (C.c_void_p * n)(*[base + i * size for i in range(n)])
@@ -63,7 +65,8 @@ def main():
                 t = statistics.median(ts)
                 print(json.dumps({"tool": "rx_verify_bench", "packet_bytes": size, "batch": n, "memory": mem,
                                   "ms_per_call": round(t * 1e3, 4), "gib_per_s": round(total / t / 2**30, 3),
-                                  "mpkt_per_s": round(n / t / 1e6, 3), "verified": int((ok == 7).sum())}), flush=True)
+                                  "mpkt_per_s": round(n / t / 1e6, 3), "verified": int((ok == 7).sum()),
+                                  "l4_checked": int(((ok & 4) != 0).sum())}), flush=True)
                 del pk, buf
                 if mem == "pinned":
                     lib.pipck_host_free(C.c_void_p(p))
