@@ -28,14 +28,14 @@ WORKLOADS = {"cfg1": 256 << 20, "cfg1p": 256 << 20, "cfg2": 4 << 20, "cfg3": 1 <
              "cfg4d": 8 << 20, "cfg4b": 8 << 20}
 
 
-def worker(only: list[str], iters: int) -> None:
+def worker(only: list[str], iters: int, warm: int = 0, b2b: bool = False) -> None:
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "tools"))
     import torch
 
     from pip_amd import engine
     from pip_amd.workloads import BY_CFG, N_FLOWS
-    from size_scan import timed
+    from size_scan import timed, timed_b2b
 
     engine.require_gpu()
     # placement probe: PIPCK_AB_PAD_MB of device memory held before the batches
@@ -73,7 +73,9 @@ def worker(only: list[str], iters: int) -> None:
             engine.gen_fixed(arena, w.stride, w.length, n, 0, w.seed, w.hdr)
             nbytes = (w.length + 2) * n
             run = lambda: engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS)  # noqa: E731
-        ms = statistics.median(timed(run, iters) for _ in range(3))
+        for _ in range(warm):  # past the GPU's post-idle clock ramp (DESIGN §5 "Warm-up")
+            run()
+        ms = statistics.median((timed_b2b if b2b else timed)(run, iters) for _ in range(3))
         digest = hashlib.sha256(run().cpu().numpy().tobytes()).hexdigest()[:16]
         tag = ("+pseudo" if fam and not w.family else "") + ("+desc" if name == "cfg4d" else "") + \
             ("+bytes" if name == "cfg4b" else "")
@@ -88,12 +90,14 @@ def main():
     ap.add_argument("--only", default="cfg2,cfg3,cfg5,cfg4")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warm", type=int, default=0, help="untimed launches per workload before timing (clock ramp: 40)")
+    ap.add_argument("--b2b", action="store_true", help="launches back to back as bench.py times them")
     ap.add_argument("--worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     only = [x for x in a.only.split(",") if x]
     if a.worker:
-        worker(only, a.iters)
+        worker(only, a.iters, a.warm, a.b2b)
         return
     # an arm is a library path, or "path@MB" / "cur@MB": that build with MB of
     # device memory allocated before its batches (a placement probe)
@@ -111,7 +115,7 @@ def main():
         for arm, (path, pad) in order:
             env = dict(os.environ, PIPCK_LIB=path, PIPCK_AB_PAD_MB=pad)
             r = subprocess.run([sys.executable, __file__, "--worker", "--only", ",".join(only), "--iters",
-                                str(a.iters)], env=env, capture_output=True, text=True, timeout=600)
+                                str(a.iters), "--warm", str(a.warm)] + (["--b2b"] if a.b2b else []), env=env, capture_output=True, text=True, timeout=600)
             if r.returncode:
                 sys.stderr.write(r.stderr[-3000:])
                 raise SystemExit(f"arm {arm} failed (rc {r.returncode})")

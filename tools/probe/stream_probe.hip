@@ -46,8 +46,18 @@ __device__ __forceinline__ i32x4 srsrc(const void* p, uint32_t bytes) {
     const uint64_t a = (uint64_t)p;
     return i32x4{(int)rfl((uint32_t)a), (int)rfl((uint32_t)(a >> 32)), (int)rfl(bytes), 0x00020000};
 }
+// POL: the load's cache-policy bits (1 = nt, 2 = sc0, 4 = sc1); the default
+// arms use nt alone, the POL arms (kind 40 + POL) sweep the combinations
+template <int POL = 1>
 __device__ __forceinline__ void ld_asm(u32x4& v, const i32x4& r, uint32_t off) {
-    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 0) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 1) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen nt" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 2) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc0" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 3) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc0 nt" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 4) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 5) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1 nt" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 6) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc0 sc1" : "=v"(v) : "v"(off), "s"(r));
+    if constexpr (POL == 7) asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc0 sc1 nt" : "=v"(v) : "v"(off), "s"(r));
 }
 template <int N>
 __device__ __forceinline__ void wait_vm(u32x4& v) {
@@ -61,12 +71,12 @@ template <int U, int OVH = 0, int G = 1>
 __device__ __forceinline__ uint32_t row_of(uint32_t j, uint32_t first, uint32_t step) {
     return ((j / G) * step + first) * G + j % G;
 }
-template <int U, int OVH = 0, int G = 1>
+template <int U, int OVH = 0, int G = 1, int POL = 1>
 __device__ __forceinline__ uint32_t stream_rows(i32x4 b, uint32_t first, uint32_t step, uint32_t nr, int lane) {
     uint32_t acc = 0;
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) ld_asm(v[u], b, (row_of<U, OVH, G>(u, first, step) * 64 + lane) * 16);
+    for (int u = 0; u < U; u++) ld_asm<POL>(v[u], b, (row_of<U, OVH, G>(u, first, step) * 64 + lane) * 16);
     for (uint32_t j = 0; j < nr; j += U) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -77,7 +87,7 @@ __device__ __forceinline__ uint32_t stream_rows(i32x4 b, uint32_t first, uint32_
                 acc = (acc ^ (uint32_t)(i * 0x9E37u)) + (acc >> 3);
                 if (i % 8 == 7 && ((j + u + i) & 1)) acc ^= rfl(acc) >> 7;  // a uniform scalar branch
             }
-            ld_asm(v[u], b, (row_of<U, OVH, G>(j + U + u, first, step) * 64 + lane) * 16);
+            ld_asm<POL>(v[u], b, (row_of<U, OVH, G>(j + U + u, first, step) * 64 + lane) * 16);
         }
     }
     wait_vm<0>(v[0]);  // drain the dummies before their registers are reused:
@@ -100,7 +110,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(wpe<U>
 }
 
 // a block task = tc chunks of 16 B
-template <int U, int WPB, int OVH = 0, int G = 1>
+template <int U, int WPB, int OVH = 0, int G = 1, int POL = 1>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(wpe<U>()))) void k_coop(
     const uint8_t* __restrict__ a, uint64_t chunks, uint32_t tc, uint32_t* out) {
     const int lane = threadIdx.x & 63;
@@ -111,7 +121,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(wpe<U>
     const uint32_t nb = (nc + 63) / 64;
     // this wave's rows: groups of G rows, groups w, w+WPB, ... (rows past the task read zeros)
     const uint32_t ng = (nb + G - 1) / G, nr = ng > w ? (ng - w + WPB - 1) / WPB * G : 0;
-    const uint32_t acc = stream_rows<U, OVH, G>(srsrc(a + c0 * 16, nc * 16), w, WPB, nr, lane);
+    const uint32_t acc = stream_rows<U, OVH, G, POL>(srsrc(a + c0 * 16, nc * 16), w, WPB, nr, lane);
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
@@ -201,13 +211,27 @@ static void launch(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out,
         hipLaunchKernelGGL((k_coop<U, WPB>), dim3((uint32_t)((rows * 64 + tc - 1) / tc)), dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
     } else if (m.kind == 5) {  // persistent coop: every wave slot the occupancy cap allows, 4-wave blocks
         hipLaunchKernelGGL((k_coop_persist<U>), dim3(cus * wpe<U>()), dim3(256), 0, 0, a, rows, m.T, out);
-    } else if (m.kind >= 10) {  // coop, rows in groups of G = kind - 10 (2, 4, 8, 16)
+    } else if (m.kind >= 10 && m.kind < 40) {  // coop, rows in groups of G = kind - 10 (2, 4, 8, 16)
         const uint32_t tc = WPB * m.T * 64 - g_skew;
         const dim3 g((uint32_t)((rows * 64 + tc - 1) / tc));
         if (m.kind == 12) hipLaunchKernelGGL((k_coop<U, WPB, 0, 2>), g, dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
         if (m.kind == 14) hipLaunchKernelGGL((k_coop<U, WPB, 0, 4>), g, dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
         if (m.kind == 18) hipLaunchKernelGGL((k_coop<U, WPB, 0, 8>), g, dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
         if (m.kind == 26) hipLaunchKernelGGL((k_coop<U, WPB, 0, 16>), g, dim3(64 * WPB), 0, 0, a, rows * 64, tc, out);
+    } else if (m.kind >= 40 && m.kind < 48) {  // coop, load cache policy kind - 40
+        const uint32_t tc = WPB * m.T * 64 - g_skew;
+        const dim3 g((uint32_t)((rows * 64 + tc - 1) / tc));
+        const dim3 b(64 * WPB);
+        switch (m.kind - 40) {
+            case 0: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 0>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 1: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 1>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 2: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 2>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 3: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 3>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 4: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 4>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 5: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 5>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            case 6: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 6>), g, b, 0, 0, a, rows * 64, tc, out); break;
+            default: hipLaunchKernelGGL((k_coop<U, WPB, 0, 1, 7>), g, b, 0, 0, a, rows * 64, tc, out); break;
+        }
     } else if (m.kind == 3 || m.kind == 4) {
         const uint32_t tc = WPB * m.T * 64 - g_skew;
         const dim3 g((uint32_t)((rows * 64 + tc - 1) / tc));
@@ -231,7 +255,7 @@ static void run(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out, ui
 int main(int argc, char** argv) {
     // sizes in GB (1e9) of 1 KiB rows; default cfg2's 6.2 GB and cfg3's 9.4 GB
     std::vector<double> sizes = {6.216, 9.4};
-    int reps = 15, rounds = 3;
+    int reps = 15, rounds = 3, warm = 3;
     std::vector<Arm> arms = {
         {"disp_u24_w4_t64", 24, 4, 64, 0},   {"disp_u32_w4_t128", 32, 4, 128, 0}, {"coop_u24_w4_t64", 24, 4, 64, 1},
         {"coop_u24_w4_t32", 24, 4, 32, 1},   {"coop_u24_w4_t128", 24, 4, 128, 1}, {"coop_u16_w4_t64", 16, 4, 64, 1},
@@ -243,6 +267,10 @@ int main(int argc, char** argv) {
         // wider blocks: 8 / 16 waves interleaved row by row over one block task
         {"coop_u24_w8_t64", 24, 8, 64, 1}, {"coop_u32_w8_t64", 32, 8, 64, 1}, {"coop_u16_w16_t64", 16, 16, 64, 1},
         {"coop_u16_w8_t64", 16, 8, 64, 1}, {"coop_u24_w8_t32", 24, 8, 32, 1},
+        // k_flat_coop's jumbo schedule (ring 32, 64 rows per wave) under every load cache policy
+        {"pol_plain", 32, 4, 64, 40}, {"pol_nt", 32, 4, 64, 41}, {"pol_sc0", 32, 4, 64, 42},
+        {"pol_sc0_nt", 32, 4, 64, 43}, {"pol_sc1", 32, 4, 64, 44}, {"pol_sc1_nt", 32, 4, 64, 45},
+        {"pol_sc0_sc1", 32, 4, 64, 46}, {"pol_sc0_sc1_nt", 32, 4, 64, 47},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";
@@ -259,6 +287,7 @@ int main(int argc, char** argv) {
         }
     }
     if (argc > 2) rounds = atoi(argv[2]);
+    if (getenv("PROBE_WARM")) warm = atoi(getenv("PROBE_WARM"));  // launches before the timed ones (clock ramp: ~30)
     if (getenv("PROBE_TASK_SKEW")) g_skew = (uint32_t)atoi(getenv("PROBE_TASK_SKEW"));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, 0));
@@ -280,7 +309,7 @@ int main(int argc, char** argv) {
             const uint64_t rows = (uint64_t)(g * 1e9) / 1024;
             for (const Arm& m : arms) {
                 std::vector<float> ms;
-                for (int i = 0; i < reps + 3; i++) {
+                for (int i = 0; i < reps + warm; i++) {
                     CK(hipMemsetAsync(ctr, 0, 4, 0));
                     CK(hipEventRecord(e0, 0));
                     run(m, a, rows, out, ctr, cus);
@@ -288,7 +317,7 @@ int main(int argc, char** argv) {
                     CK(hipEventSynchronize(e1));
                     float t;
                     CK(hipEventElapsedTime(&t, e0, e1));
-                    if (i >= 3) ms.push_back(t);
+                    if (i >= warm) ms.push_back(t);
                 }
                 CK(hipGetLastError());
                 std::sort(ms.begin(), ms.end());
