@@ -92,4 +92,12 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
 int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint16_t* d_out,
                uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags, bool coop = false);
 
+// The one-packet-per-wave measurement arm (pipck_wave.hip; pipck_tune
+// lanes_per_packet == kWaveArm): fixed strides (desc == false) or descriptors.
+constexpr uint32_t kWaveArm = 256;
+int launch_wave(bool verify, bool desc, const void* d_arena, uint64_t stride, uint32_t len, const pipck_desc* d_desc,
+                uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s,
+                uint32_t max_chunks, uint32_t nl);
+
 }  // namespace pipck

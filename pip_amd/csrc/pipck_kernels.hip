@@ -1606,6 +1606,9 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         set_error("pipck_checksum_fixed: stride < len");
         return PIPCK_EINVAL;
     }
+    if (g_tune.lanes.load() == kWaveArm)  // measurement arm: one packet per wave (pipck_wave.hip)
+        return launch_wave(verify, false, d_arena, stride, len, nullptr, n, d_pseudo, n_flows, d_flow_of, flow_origin,
+                           d_out, d_ok, nullptr, as_stream(stream), (len + 30u) / 16u, g_tune.loads.load());
     const bool aligned = ((uintptr_t)d_arena % 16 == 0) && (stride % 16 == 0);
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
@@ -1788,6 +1791,9 @@ static void launch_ragged_u(bool final_, bool nt, uint64_t tiles, hipStream_t s,
 static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_desc, uint64_t n,
                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint8_t* d_ok, uint32_t* d_err,
                          hipStream_t s) {
+    if (final_ && !d_fseg && g_tune.lanes.load() == kWaveArm)  // measurement arm: one packet per wave
+        return launch_wave(d_ok != nullptr, true, d_arena, 0, 0, d_desc, n, d_pseudo, 1u, nullptr, 0, d_out, d_ok, d_err,
+                           s, 0, g_tune.loads.load() ? g_tune.loads.load() : 4u);
     const uint64_t tiles = (n + 63) / 64;
     // loads_per_lane: 2/4/8/16 rows in flight on packed tiles (at most 4 on
     // others), 3/5/7/9/13/17/25/33 = ring-pipelined 2/4/6/8/12/16/24/32.

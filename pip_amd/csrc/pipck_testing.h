@@ -20,7 +20,10 @@ extern "C" {
 
 /* Launch-shape override for tuning; 0 = automatic everywhere (process-wide, internal).
  * lanes_per_packet in {1,2,4,8,16,32,64} and loads_per_lane pick the fixed
- * kernel's shape (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
+ * kernel's shape; lanes_per_packet = 256 selects k_wave (pipck_wave.hip: one
+ * packet per wavefront, the north_star's sketch, a measurement arm) for fixed
+ * strides and descriptor batches, loads_per_lane 2/4/8/16 its chunks per lane
+ * per pass (loads_per_lane in {2,4,8} also sets the ragged kernel's rows
  * in flight; for the flat-stream kernel 2/4/8/16 rows, 3/5/9/13/17/25/33 =
  * ring-pipelined 2/4/8/12/16/24/32); blocks caps the grid; flags bit 0 = plain (cached) loads, bit 2 =
  * non-temporal loads (default: per kernel), bit 1 = never use the flat-stream

@@ -332,7 +332,7 @@ LENGTHS = [0, 1, 2, 3, 15, 16, 17, 20, 31, 33, 64, 100, 1023, 1024, 1025, 1480, 
            20001, 65535]
 
 
-@pytest.mark.parametrize("lanes", [0, 1, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("lanes", [0, 1, 2, 4, 8, 16, 32, 64, 256])  # 256: k_wave, one packet per wave
 def test_fixed_every_shape_vs_oracle(oracle, lanes):
     rng = np.random.default_rng(100 + lanes)
     engine.tune(lanes)
@@ -351,6 +351,8 @@ def test_fixed_every_shape_vs_oracle(oracle, lanes):
                 seed, proto, origin = int(rng.integers(0, 2**63)), int(rng.integers(0, 256)), int(rng.integers(0, 5000))
                 pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
                 out = engine.checksum_fixed(arena, stride, length, n, pseudo, N_FLOWS, None, origin)
+                if lanes == 256:
+                    assert "k_wave<" in last_kernel()
                 want = oracle.batch_fixed(host, stride, length, n, fam, proto, seed, N_FLOWS, origin)
                 got = u16(out)
                 assert np.array_equal(got, want), (lanes, length, stride, fam, misalign,
@@ -901,6 +903,43 @@ def test_ragged_tiny_segment_tiles(oracle, misalign):
             assert np.array_equal(got, want), (tiny, np.nonzero(got != want)[0][:5])
             ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy().astype(bool)
             assert np.array_equal(ok, got == 0)
+    finally:
+        engine.tune()
+
+
+@pytest.mark.parametrize("nl", [0, 2, 16])
+def test_wave_per_packet_arm_ragged_vs_oracle(oracle, nl):
+    """k_wave (pipck_wave.hip, the north_star's one-packet-per-wavefront shape,
+    a measurement arm behind tune lanes_per_packet=256) on descriptor batches:
+    unaligned, permuted, empty and 65,535-byte segments, several passes per
+    packet (nl 2 = 2 KiB per pass), RX verify."""
+    rng = np.random.default_rng(300 + nl)
+    engine.tune(256, nl)
+    try:
+        for fam, max_len in ((4, 9000), (6, 65535), (0, 300)):
+            n = int(rng.integers(500, 1500))
+            offs, lens, size = _ragged_case(rng, n, max_len)
+            host = rng.integers(0, 256, size + 16, dtype=np.uint8)
+            _, arena = upload(host, int(rng.integers(0, 16)))
+            seed, proto, origin = 77 + nl, 17, int(rng.integers(0, 999))
+            pseudo = engine.gen_flows(fam, N_FLOWS, seed, proto)[1] if fam else None
+            desc = engine.make_desc(offs, lens, (origin + np.arange(n)) % N_FLOWS)
+            got = u16(engine.checksum_ragged(arena, desc, pseudo))
+            assert "k_wave<" in last_kernel()
+            want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
+            assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
+            ok = engine.verify_ragged(arena, desc, pseudo).cpu().numpy().astype(bool)
+            assert np.array_equal(ok, got == 0)
+        # out of the batch domain: 0 and PIPCK_ERANGE, as k_ragged
+        offs = np.array([0, 10, 100_000, 5], dtype=np.uint64)
+        lens = np.array([100, 70_000, 33, 0], dtype=np.uint32)
+        host = rng.integers(0, 256, 200_000, dtype=np.uint8)
+        _, arena = upload(host)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        got = u16(engine.checksum_ragged(arena, engine.make_desc(offs, lens, np.zeros(4)), None, err=err))
+        assert int(err.item()) & (1 << _lib.PIPCK_ERANGE) and got[1] == 0
+        for i in (0, 2, 3):
+            assert got[i] == oracle.ip_checksum(host[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
     finally:
         engine.tune()
 
