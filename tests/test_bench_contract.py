@@ -156,25 +156,26 @@ shard.shutdown(env)
 @pytest.mark.parametrize("world", [2, 4])
 def test_injected_start_skew_lowers_the_aggregate(tmp_path, capfd, world):
     """gloo ranks on one host whose timed starts are skewed after the barrier
-    (rank r waits r x 60 ms, as bench.py --start-skew-ms does): the reported
+    (rank r waits r x 200 ms, as bench.py --start-skew-ms does): the reported
     aggregate drops by the skew, while the max-over-ranks elapsed time would
-    not see it.  Unskewed, the two agree."""
+    not see it.  Unskewed, the two agree within the scheduling noise of
+    several processes on a busy CPU (a 50-ms bound failed once under pytest -n 4)."""
     import json
     import sys
     from pathlib import Path
 
     root = str(Path(__file__).resolve().parents[1])
     got = {}
-    for skew in (0.0, 0.06):
+    for skew in (0.0, 0.2):
         script = tmp_path / f"skew{skew}.py"
         script.write_text(_SKEW_SCRIPT.format(root=root, skew=skew))
         assert shard.spawn_ranks(world, [sys.executable, str(script)]) == 0
         out = capfd.readouterr().out
         got[skew] = json.loads(next(ln for ln in out.splitlines() if ln.startswith("AGG "))[4:])
-    flat, skewed = got[0.0], got[0.06]
-    want_skew = (world - 1) * 60
-    assert flat["start_skew_ms"] < 50 and flat["span_s"] < flat["max_rank_s"] + 0.05
-    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 100
+    flat, skewed = got[0.0], got[0.2]
+    want_skew = (world - 1) * 200
+    assert flat["start_skew_ms"] < 150 and flat["span_s"] < flat["max_rank_s"] + 0.15
+    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 150
     assert skewed["span_s"] >= skewed["max_rank_s"] + (want_skew - 5) / 1e3
     assert skewed["rate"] < 0.75 * skewed["rate_max_rank"]
     assert skewed["rate"] == pytest.approx(world * 1e9 * 5 / skewed["span_s"])
