@@ -160,3 +160,59 @@ def test_workload_text_states_the_real_count():
     assert CFG1.describe(256 << 20) .endswith("256M packets")
     assert CFG1.describe(1000).endswith("1,000 packets")
     assert CFG1.stride == 20 == CFG1.length  # packed headers: no slot padding
+
+
+_N8_SCRIPT = """
+import json, socket, sys, time
+sys.path.insert(0, {root!r})
+from pip_amd import shard
+env = shard.dist_env()
+shard.init_control_plane(env)
+# bench.py's run_rank on an 8-GPU node, minus the GPU: device choice, timed
+# region, the gathers and the aggregate, in bench.py's order
+dev = shard.device_for_rank(env.local_rank, shard.local_world_size(env), 8, False)
+place = {{"rank": env.rank, "host": socket.gethostname(), "device": dev, "pci_bus_id": "0000:%02x:00.0" % (16 * dev)}}
+t0, t1 = shard.timed_steps(env, 5, lambda i: time.sleep(0.01), lambda: None)
+ranks = shard.gather_over_ranks(env, [1e9, 1000.0, (t1 - t0) / 1e9, 0.002])
+clocks = shard.gather_ints(env, [t0, t1])
+places = shard.gather_objects(env, place)
+agg = shard.aggregate([c[0] for c in clocks], [c[1] for c in clocks], [r[0] for r in ranks], 5)
+shard.barrier(env)
+if env.rank == 0:
+    print("N8 " + json.dumps({{"world": env.world, "local_world": shard.local_world_size(env), "agg": agg,
+                              "devices": [p["device"] for p in places],
+                              "distinct": len({{(p["host"], p["pci_bus_id"]) for p in places}})}}), flush=True)
+shard.shutdown(env)
+"""
+
+
+@pytest.mark.parametrize("launcher", ["spawn", "torchrun"])
+def test_eight_rank_control_plane_rehearsal(tmp_path, capfd, launcher):
+    """The N=8 SCALE line's control plane on CPU (gloo, 8 processes): each local
+    rank takes its own device of an 8-GPU node, the gathers return all eight
+    ranks, and the aggregate is 8 shards' bytes over the shared-clock span --
+    self-launched (bench.py --gpus 8) and under torch.distributed.run as the
+    driver launches it."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parents[1])
+    script = tmp_path / "n8.py"
+    script.write_text(_N8_SCRIPT.format(root=root))
+    if launcher == "spawn":
+        assert shard.spawn_ranks(8, [sys.executable, str(script)]) == 0
+        out = capfd.readouterr().out
+    else:
+        r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                            "--master-addr", "127.0.0.1", "--master-port", str(shard.free_port()), str(script)],
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = r.stdout
+    got = json.loads(next(ln for ln in out.splitlines() if ln.startswith("N8 "))[3:])
+    assert got["world"] == 8 and got["local_world"] == 8
+    assert got["devices"] == list(range(8)) and got["distinct"] == 8
+    agg = got["agg"]
+    assert agg["span_s"] >= agg["max_rank_s"] > 0.04
+    assert agg["rate"] == pytest.approx(8 * 1e9 * 5 / agg["span_s"])
