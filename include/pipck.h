@@ -397,6 +397,21 @@ int pipck_rxq_destroy(pipck_rxq* q);
 int pipck_rx_verify(pipck_rxq* q, const void* const* pkts, const uint32_t* lens, uint64_t n, uint8_t* ok,
                     uint64_t* n_verified);
 
+/* The same verdicts for received IP packets already in DEVICE memory, in the
+ * byte-packed layout of pipck_checksum_packed_bytes (frame i of d_lens[i]
+ * bytes at d_arena + b_i, d_tile_off from pipck_packed_bytes_index; link
+ * padding after the IP length allowed): d_ok[i] gets the PIPCK_RX_* bits
+ * pipck_rx_verify gives the same bytes.  One kernel on `stream`, no host
+ * work: the byte-packed stream sums every frame once, then a lane per packet
+ * parses its headers and derives the IP-header and payload verdicts from that
+ * sum.  The arena must be 128-byte aligned and readable to the 16-byte
+ * boundary after the last frame.  Bounded as pipck_checksum_packed_bytes_n: a tile
+ * reaching past arena_bytes is not read, its packets get 0 and d_err
+ * (optional) gets (1 << PIPCK_ERANGE).  Asynchronous. */
+int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                           const uint64_t* d_tile_off, uint64_t n_packets, uint8_t* d_ok, uint32_t* d_err,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

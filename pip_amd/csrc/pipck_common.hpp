@@ -92,6 +92,10 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
 int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, uint16_t* d_out,
                uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags, bool coop = false);
 
+// pipck_rx_verify_device (pipck_packedb.hip): k_packedb with the RX verdicts.
+int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens, const uint64_t* d_tile_off,
+                      uint64_t n, uint8_t* d_ok, uint32_t* d_err, hipStream_t s);
+
 // The one-packet-per-wave measurement arm (pipck_wave.hip; pipck_tune
 // lanes_per_packet == kWaveArm): fixed strides (desc == false) or descriptors.
 constexpr uint32_t kWaveArm = 256;

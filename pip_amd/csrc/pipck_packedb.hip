@@ -29,6 +29,7 @@
 // lengths (0 included), slow, and absent from the BASELINE shapes (>= 64 B).
 #include "pipck_common.hpp"
 #include "pipck_device.hpp"
+#include "pipck_rxparse.hpp"
 
 namespace pipck {
 
@@ -158,14 +159,17 @@ __device__ __forceinline__ uint32_t packedb_lane_sum(uintptr_t base, uint32_t st
     return acc;
 }
 
-template <bool VERIFY, int U, bool NT>
-__global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
-                                                const uint64_t* __restrict__ tile_off, uint64_t n,
-                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
-                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                uint64_t arena_bytes, uint32_t* __restrict__ err) {
-    __shared__ PackedbLds t;
+// The kernel body.  RX = true (k_packedb_rx: pipck_rx_verify_device,
+// pipck_rxdev.hip): each frame's sum feeds rx_device_one (pipck_rxparse.hpp) at
+// the tile's end and the ok byte carries the PIPCK_RX_* bits (VERIFY true, no
+// pseudo-header).
+template <bool VERIFY, int U, bool NT, bool RX>
+__device__ __forceinline__ void packedb_body(PackedbLds& t, const uint8_t* __restrict__ arena,
+                                             const uint16_t* __restrict__ lens, const uint64_t* __restrict__ tile_off,
+                                             uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                             const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                             uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                             uint64_t arena_bytes, uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const uint64_t tile = blockIdx.x;
     const uint64_t seg = tile * 64 + lane;
@@ -220,11 +224,39 @@ __global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ aren
     const uint32_t w = fold16(le);
     const uint32_t F = (start & 1u) ? w : bswap16(w);  // byte order from the packet's start parity
     const uint32_t P = pseudo ? Pbase + len : 0u;
-    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    uint32_t r;
+    if (RX)  // the frame's own headers, from the lines this tile just streamed
+        r = valid ? rx_device_one(reinterpret_cast<const uint8_t*>(base + start), len, F) : 0u;
+    else
+        r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
     if (VERIFY)  // write-through result stores (store_result16); lanes past the batch are range-checked off
         store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, r);
     else
         store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, r);
+}
+
+template <bool VERIFY, int U, bool NT>
+__global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
+                                                const uint64_t* __restrict__ tile_off, uint64_t n,
+                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                uint64_t arena_bytes, uint32_t* __restrict__ err) {
+    __shared__ PackedbLds t;
+    packedb_body<VERIFY, U, NT, false>(t, arena, lens, tile_off, n, pseudo, n_flows, flow_of, flow_origin, out, ok,
+                                       arena_bytes, err);
+}
+
+// received IP frames: the stream, then each tile's headers parsed and judged
+template <int U, bool NT>
+__global__ __launch_bounds__(64) void k_packedb_rx(const uint8_t* __restrict__ arena,
+                                                   const uint16_t* __restrict__ lens,
+                                                   const uint64_t* __restrict__ tile_off, uint64_t n,
+                                                   uint8_t* __restrict__ ok, uint64_t arena_bytes,
+                                                   uint32_t* __restrict__ err) {
+    __shared__ PackedbLds t;
+    packedb_body<true, U, NT, true>(t, arena, lens, tile_off, n, nullptr, 1u, nullptr, 0, nullptr, ok, arena_bytes,
+                                    err);
 }
 
 // tile_off[t] = bytes of every packet before packet 64 t (the last entry = the
@@ -292,6 +324,30 @@ static int launch_packedb(bool verify, const void* d_arena, uint64_t arena_bytes
                           (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
                           d_ok, arena_bytes, d_err);
     PIPCK_LAUNCHED("k_packedb");
+    return PIPCK_OK;
+}
+
+// pipck_rx_verify_device: the byte-packed stream with the RX verdicts at each
+// tile's end (argument checks as pipck_checksum_packed_bytes)
+int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens, const uint64_t* d_tile_off,
+                      uint64_t n, uint8_t* d_ok, uint32_t* d_err, hipStream_t s) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_lens || !d_tile_off || !d_ok) {
+        set_error("pipck_rx_verify_device: null pointer");
+        return PIPCK_EINVAL;
+    }
+    if ((uintptr_t)d_arena % 128) {
+        set_error("pipck_rx_verify_device: the arena must be 128-byte aligned");
+        return PIPCK_EINVAL;
+    }
+    const uint64_t tiles = (n + 63) / 64;
+    if (tiles > 0x7FFFFFFFull) {
+        set_error("pipck_rx_verify_device: more than 2^37 packets in one launch");
+        return PIPCK_ERANGE;
+    }
+    PIPCK_LAUNCH((k_packedb_rx<32, true>), dim3((uint32_t)tiles), dim3(64), 0, s, (const uint8_t*)d_arena, d_lens,
+                 d_tile_off, n, d_ok, arena_bytes, d_err);
+    PIPCK_LAUNCHED("k_packedb_rx");
     return PIPCK_OK;
 }
 

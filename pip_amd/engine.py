@@ -234,6 +234,20 @@ def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None
     return ok
 
 
+def rx_verify_device(arena, lens, tile_off, n: int | None = None, ok=None, err=None):
+    """Received IP packets in device memory, byte-packed (pipck_rx_verify_device): the
+    PIPCK_RX_* bits per packet (uint8), as pipck_rx_verify gives for the same bytes in
+    host memory.  Tiles are bounded by the arena's size on the device (err as checksum_packed)."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
+    _check_packed(arena, lens, tile_off, n, unit=1)
+    call("pipck_rx_verify_device", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(ok), _ptr(err),
+         current_stream(arena.device))
+    return ok
+
+
 def packed_bytes_index(lens, n: int | None = None):
     """tile_off for a byte-packed batch: the byte offset of every 64th packet (u64 as int64) + the total."""
     torch = _torch()

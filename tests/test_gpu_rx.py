@@ -113,3 +113,141 @@ def test_rx_verify_c_abi_edges(oracle):
         assert lib.pipck_rx_verify(q, None, None, 1, ok8.ctypes.data, None) == _lib.PIPCK_EINVAL
     finally:
         lib.pipck_rxq_destroy(q)
+
+
+# ---- pipck_rx_verify_device: the same packets already in device memory ---------
+def _device_batch(frames):
+    """Frames back to back in a device arena (the byte-packed layout), u16 lengths, tile index."""
+    import torch
+
+    from pip_amd import engine
+
+    total = sum(len(f) for f in frames)
+    buf = np.zeros(total + 32, dtype=np.uint8)  # readable past the last frame's 16-byte chunk
+    off = 0
+    for f in frames:
+        buf[off:off + len(f)] = np.frombuffer(f, dtype=np.uint8)
+        off += len(f)
+    arena = torch.from_numpy(buf).to("cuda")
+    lens = torch.from_numpy(np.array([len(f) for f in frames], dtype=np.uint16).view(np.int16)).to("cuda")
+    return arena, lens, engine.packed_bytes_index(lens)
+
+
+def _ipv4(oracle, proto, l4, src=b"\x0a\0\0\x01", dst=b"\x0a\0\0\x02"):
+    import struct
+
+    hdr = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, 20 + len(l4), 7, 0, 64, proto, 0, src, dst))
+    c = oracle.ip_checksum(bytes(hdr))
+    hdr[10:12] = struct.pack(">H", c)
+    return bytes(hdr) + bytes(l4)
+
+
+@pytest.mark.gpu
+def test_rx_verify_device_equals_host_path(oracle):
+    """pipck_rx_verify_device (packets in HBM, parsed on the GPU, payload sums
+    derived from the k_packedb stream's frame sums) gives exactly the bits the host-parsed
+    pipck_rx_verify gives, on 5,000 oracle-checksummed IPv4/IPv6
+    TCP/UDP/ICMP packets up to 64 KB with damage in the header, the payload or
+    the checksum field and link padding after the IP length."""
+    import torch
+
+    from pip_amd import engine
+
+    rng = random.Random(202)
+    pkts, want = [], []
+    for k in range(5000):
+        fam = rng.choice([4, 6])
+        proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
+        l4len = rng.choice([rng.randint(20, 1500), rng.randint(8000, 9000), rng.randint(60000, 65400)]) \
+            if k % 50 == 0 else rng.randint(20, 1500)
+        p = bytearray(_rx_packet(oracle, rng, fam, proto, l4len, k + 1))
+        checked = not (fam == 4 and proto == 17 and (k + 1) % 7 == 0)
+        w = VERIFIED if checked else UNCHECKED
+        hl = 20 if fam == 4 else 40
+        if k % 4 == 1 and checked:
+            i = rng.randrange(hl, len(p))
+            if fam == 4 and proto == 17 and i in (hl + 6, hl + 7):
+                i = hl
+            p[i] ^= 0x08
+            w = IP_OK | L4_CHECKED
+        elif k % 4 == 2 and fam == 4:
+            p[rng.choice([1, 4, 5, 8, 10, 11])] ^= 0x40
+            w &= ~IP_OK
+        pkts.append(bytes(p) + rng.randbytes(rng.choice([0, 3, 17])))
+        want.append(w)
+    arena, lens, tile_off = _device_batch(pkts)
+    ok = engine.rx_verify_device(arena, lens, tile_off).cpu().numpy()
+    assert list(ok) == want
+    assert (np.array(want) == VERIFIED).sum() > 1000
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_rx_verify_device_edges(oracle):
+    """Frames the GPU parser must treat as the host parser does: empty, short,
+    malformed and non-IP frames; IPv6 extension headers inside and past the
+    80-byte register window; fragments and routing headers (unchecked); UDP
+    over IPv4 without a checksum; a truncated TCP header; long link padding; and
+    ICMPv4 without a pseudo-header -- an all-zero message with a zero field
+    fails (its checksum is 0xFFFF), while a message whose first 8 bytes are zero
+    but whose payload sums to 0xFFFF verifies.  Every verdict equals the host
+    path's (pipck_rx_verify on the same bytes)."""
+    from pip_amd import engine
+
+    rng = random.Random(5)
+    zero_icmp = _ipv4(oracle, 1, bytes(8))                        # T = 0: checksum should be 0xFFFF
+    ffff_icmp = _ipv4(oracle, 1, bytes(8) + b"\xff\xff")          # T = 0xFFFF: checksum 0, verifies
+    cases = [
+        (b"", 0), (bytes(19), 0), (bytes([0x45]) + bytes(30), 0), (bytes([0x55]) + bytes(60), 0),
+        (_rx_packet(oracle, rng, 6, 6, 200, 1, ext=_ext([(0, 0), (60, 1)], 6)), VERIFIED),
+        (_rx_packet(oracle, rng, 6, 17, 300, 2, ext=_ext([(0, 20), (60, 3)], 17)), VERIFIED),  # past 80 B
+        (_rx_packet(oracle, rng, 6, 58, 64, 3, ext=_ext([(44, 0)], 58)), VERIFIED),   # atomic fragment
+        (_rx_packet(oracle, rng, 6, 17, 200, 4, ext=_ext([(44, 0x0001)], 17)), UNCHECKED),
+        (_rx_packet(oracle, rng, 6, 6, 200, 5, ext=_ext([(43, 0)], 6)), UNCHECKED),   # routing header
+        (_rx_packet(oracle, rng, 4, 6, 40, 6, frag=0x2000), UNCHECKED),
+        (_rx_packet(oracle, rng, 4, 17, 100, 7), UNCHECKED),                          # k % 7 == 0: no UDP sum
+        (_rx_packet(oracle, rng, 4, 1, 8, 8), VERIFIED),
+        (_rx_packet(oracle, rng, 4, 6, 40, 9)[:20 + 12], None),                       # truncated TCP
+        (_rx_packet(oracle, rng, 4, 6, 20, 10) + bytes(100), VERIFIED),               # long link padding
+        (_rx_packet(oracle, rng, 6, 6, 20, 11) + rng.randbytes(90), VERIFIED),
+        (zero_icmp, IP_OK | L4_CHECKED), (ffff_icmp, VERIFIED),
+    ]
+    frames = [p for p, _ in cases]
+    lib, q = _rxq()
+    try:
+        bufs = [C.create_string_buffer(p, max(len(p), 1)) for p in frames]
+        host = _run(lib, q, [C.cast(b, C.c_void_p).value for b in bufs], [len(p) for p in frames])
+    finally:
+        lib.pipck_rxq_destroy(q)
+    arena, lens, tile_off = _device_batch(frames)
+    dev = engine.rx_verify_device(arena, lens, tile_off).cpu().numpy()
+    assert list(dev) == list(host)
+    for (p, w), got in zip(cases, dev):
+        if w is not None:
+            assert got == w, (p[:48].hex(), got, w)
+
+
+@pytest.mark.gpu
+def test_rx_verify_device_bounded_by_the_arena(oracle):
+    """A tile index that claims more bytes than the arena holds: that tile is
+    not read, its packets get 0 and PIPCK_ERANGE is set (no Python guard: the
+    C ABI directly)."""
+    import torch
+
+    from pip_amd import _lib
+
+    rng = random.Random(9)
+    frames = [_rx_packet(oracle, rng, 4, 6, 500, k + 1) for k in range(130)]
+    arena, lens, tile_off = _device_batch(frames)
+    n = len(frames)
+    ok = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    short = int(tile_off[1].item()) + 10  # tile 0 fits, tiles 1 and 2 do not
+    lib = _lib.load()
+    rc = lib.pipck_rx_verify_device(arena.data_ptr(), short, lens.data_ptr(), tile_off.data_ptr(), n,
+                                    ok.data_ptr(), err.data_ptr(), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = ok.cpu().numpy()
+    assert (got[:64] == VERIFIED).all() and (got[64:] == 0).all()
+    assert int(err.item()) & (1 << _lib.PIPCK_ERANGE)
