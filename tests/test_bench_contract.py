@@ -175,7 +175,10 @@ def test_injected_start_skew_lowers_the_aggregate(tmp_path, capfd, world):
     flat, skewed = got[0.0], got[0.2]
     want_skew = (world - 1) * 200
     assert flat["start_skew_ms"] < 150 and flat["span_s"] < flat["max_rank_s"] + 0.15
-    assert want_skew - 5 < skewed["start_skew_ms"] < want_skew + 150
-    assert skewed["span_s"] >= skewed["max_rank_s"] + (want_skew - 5) / 1e3
+    assert want_skew - 50 < skewed["start_skew_ms"] < want_skew + 150
+    # the span covers the skew and a whole rank's run (the slowest rank need
+    # not be the late starter on a busy CPU, so not max_rank_s + skew)
+    assert skewed["span_s"] >= skewed["start_skew_ms"] / 1e3 + 0.1 - 0.005
+    assert skewed["span_s"] > skewed["max_rank_s"] + 0.1
     assert skewed["rate"] < 0.75 * skewed["rate_max_rank"]
     assert skewed["rate"] == pytest.approx(world * 1e9 * 5 / skewed["span_s"])
