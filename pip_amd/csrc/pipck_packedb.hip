@@ -56,7 +56,17 @@ __device__ __forceinline__ void packedb_flush(PackedbLds& t, int lane, uint32_t&
 // the first chunk whose first byte lies in packet s (start rounded up to 16);
 // nv valid packets.  S0 / e0: the slot holding the row's first byte and its
 // end byte (scalars, carried across rows).
-__device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, uint32_t row, uint32_t total, int lane,
+//
+// RX (k_packedb_rx): the row also hands every packet the chunks of its header
+// window -- the six aligned chunks from the one holding its first byte, as far
+// as the packet reaches -- into hdr[k * 64 + packet] in LDS, so the tile's end
+// parses headers without reading them from memory again.  A chunk whose first
+// byte lies in packet s is window chunk k = c - (start_s >> 4) of s when
+// k < 6; a chunk holding a packet boundary is window chunk 0 of the packet
+// that starts inside it.  (Tiles with a packet under 16 bytes take the
+// lane-per-segment path and read their headers from memory.)
+template <bool RX>
+__device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, u32x4* hdr, uint32_t row, uint32_t total, int lane,
                                                    const u32x4& v, uint32_t start_v, uint32_t end_v,
                                                    uint32_t mfirst_v, bool valid, uint32_t nv, uint32_t& S0,
                                                    uint32_t& e0, uint32_t& racc, uint32_t& rslot) {
@@ -74,6 +84,13 @@ __device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, uint32_t row, 
             rslot = S0;
         }
         racc = dot4(v, racc);
+        if (RX && S0 >= 1 && S0 <= nv) {  // the row may hold the last chunks of packet S0 - 1's window
+            const uint32_t cs = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t.end[S0 - 1] >> 4));
+            if (row < cs + 6u) {  // wave-uniform
+                const uint32_t k = row + (uint32_t)lane - cs;
+                if (k < 6u) hdr[k * 64u + S0 - 1] = v;
+            }
+        }
         return;
     }
     // the run of whole rows ends here: its wave total joins S0's tail lane
@@ -108,12 +125,19 @@ __device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, uint32_t row, 
     const uint32_t add = (tail ? inc + (S == S0 ? R : 0u) : 0u) - (hd ? inc - lo : 0u);
     if (tail || hd) atomicAdd(&t.acc[S], add);
     if (active && p < 16) atomicAdd(&t.acc[S + 1], val - lo);
+    if (RX && active) {
+        if (S >= 1 && S <= nv) {  // the chunk's first byte is in packet S - 1
+            const uint32_t k = c - (t.end[S - 1] >> 4);
+            if (k < 6u) hdr[k * 64u + S - 1] = v;
+        }
+        if (p < 16 && S < nv) hdr[S] = v;  // packet S starts inside this chunk: its window chunk 0
+    }
     (void)end_v;
     (void)nv;
 }
 
-template <int U, bool NT>
-__device__ __forceinline__ void packedb_stream(PackedbLds& t, uint32_t total, int lane, uintptr_t base,
+template <int U, bool NT, bool RX>
+__device__ __forceinline__ void packedb_stream(PackedbLds& t, u32x4* hdr, uint32_t total, int lane, uintptr_t base,
                                                uint32_t start_v, uint32_t end_v, uint32_t mfirst_v, bool valid,
                                                uint32_t nv) {
     if (!total) return;
@@ -132,8 +156,8 @@ __device__ __forceinline__ void packedb_stream(PackedbLds& t, uint32_t total, in
         for (int u = 0; u < U; u++) {
             const uint32_t row = c0 + u * 64;
             if (row < total)  // wave-uniform
-                packedb_reduce_row(t, row, total, lane, v[u], start_v, end_v, mfirst_v, valid, nv, S0, e0, racc,
-                                   rslot);
+                packedb_reduce_row<RX>(t, hdr, row, total, lane, v[u], start_v, end_v, mfirst_v, valid, nv, S0, e0,
+                                       racc, rslot);
             // unconditional reload (past the tile: zeros, no request), so each
             // reduce waits for its own row only (vmcnt(U-1))
             v[u] = buf_load<NT>(tb, (row + 64u * U + lane) * 16u);
@@ -164,7 +188,7 @@ __device__ __forceinline__ uint32_t packedb_lane_sum(uintptr_t base, uint32_t st
 // the tile's end and the ok byte carries the PIPCK_RX_* bits (VERIFY true, no
 // pseudo-header).
 template <bool VERIFY, int U, bool NT, bool RX>
-__device__ __forceinline__ void packedb_body(PackedbLds& t, const uint8_t* __restrict__ arena,
+__device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const uint8_t* __restrict__ arena,
                                              const uint16_t* __restrict__ lens, const uint64_t* __restrict__ tile_off,
                                              uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                              const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
@@ -212,12 +236,13 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, const uint8_t* __res
     t.mark[lane] = 0;
     wave_sync();
     uint32_t le;
-    if (__any(valid && len < 16)) {
+    const bool lane_path = __any(valid && len < 16);
+    if (lane_path) {
         le = valid ? packedb_lane_sum(base, start, len) : 0u;
     } else {
         const uint32_t mfirst = (start + 15u) >> 4;  // first chunk whose first byte is in this packet
         const uint32_t total = (end_last + 15u) >> 4;
-        packedb_stream<U, NT>(t, total, lane, base, start, end, mfirst, valid, nv);
+        packedb_stream<U, NT, RX>(t, hdr, total, lane, base, start, end, mfirst, valid, nv);
         wave_sync();
         le = t.acc[lane + 1];
     }
@@ -225,9 +250,20 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, const uint8_t* __res
     const uint32_t F = (start & 1u) ? w : bswap16(w);  // byte order from the packet's start parity
     const uint32_t P = pseudo ? Pbase + len : 0u;
     uint32_t r;
-    if (RX)  // the frame's own headers, from the lines this tile just streamed
-        r = valid ? rx_device_one(reinterpret_cast<const uint8_t*>(base + start), len, F) : 0u;
-    else
+    if (RX) {  // the frame's header window: captured from the stream, or (lane path) read again
+        const uint8_t* pk = reinterpret_cast<const uint8_t*>(base + start);
+        uint32_t hw[24];
+        if (lane_path) {
+            rx_window_global(pk, len, hw);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 6; k++) {  // chunks past the packet's last one: zero (never captured)
+                const u32x4 x = 16u * k < (start & 15u) + len ? hdr[k * 64 + lane] : u32x4{0u, 0u, 0u, 0u};
+                hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
+            }
+        }
+        r = valid ? rx_from_window(pk, len, F, hw) : 0u;
+    } else
         r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
     if (VERIFY)  // write-through result stores (store_result16); lanes past the batch are range-checked off
         store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, r);
@@ -243,8 +279,8 @@ __global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ aren
                                                 uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
                                                 uint64_t arena_bytes, uint32_t* __restrict__ err) {
     __shared__ PackedbLds t;
-    packedb_body<VERIFY, U, NT, false>(t, arena, lens, tile_off, n, pseudo, n_flows, flow_of, flow_origin, out, ok,
-                                       arena_bytes, err);
+    packedb_body<VERIFY, U, NT, false>(t, nullptr, arena, lens, tile_off, n, pseudo, n_flows, flow_of, flow_origin,
+                                       out, ok, arena_bytes, err);
 }
 
 // received IP frames: the stream, then each tile's headers parsed and judged
@@ -255,8 +291,9 @@ __global__ __launch_bounds__(64) void k_packedb_rx(const uint8_t* __restrict__ a
                                                    uint8_t* __restrict__ ok, uint64_t arena_bytes,
                                                    uint32_t* __restrict__ err) {
     __shared__ PackedbLds t;
-    packedb_body<true, U, NT, true>(t, arena, lens, tile_off, n, nullptr, 1u, nullptr, 0, nullptr, ok, arena_bytes,
-                                    err);
+    __shared__ u32x4 hdr[6 * 64];  // header windows: chunk k of packet s at hdr[k * 64 + s]
+    packedb_body<true, U, NT, true>(t, hdr, arena, lens, tile_off, n, nullptr, 1u, nullptr, 0, nullptr, ok,
+                                    arena_bytes, err);
 }
 
 // tile_off[t] = bytes of every packet before packet 64 t (the last entry = the

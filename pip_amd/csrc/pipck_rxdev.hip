@@ -11,11 +11,10 @@
 //
 //  1. the tile's stream, unchanged, leaves each packet's folded big-endian sum
 //     S_all over its whole frame, relative to the packet's first byte;
-//  2. at the tile's end, each lane takes its packet (rx_device_one,
-//     pipck_rxparse.hpp): it reads the first 96 bytes of the packet again (up
-//     to six 16-byte loads; the stream's non-temporal lines have mostly left
-//     L2 by then: +15 % fetched bytes), realigns them to
-//     the packet start in registers, parses
+//  2. while the rows stream by, the chunks of every packet's header window
+//     (its first six aligned 16-byte chunks) are also copied to LDS; at the
+//     tile's end each lane takes its packet's window from there (rx_from_window,
+//     pipck_rxparse.hpp), realigns it to the packet start in registers, parses
 //     the fields pipck_rx_verify's host parser reads (rx_parse: IHL, lengths,
 //     fragment field, protocol, the IPv6 extension-header walk, addresses),
 //     sums the IPv4 header exactly, and gets the L4 message's sum without

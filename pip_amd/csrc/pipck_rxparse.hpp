@@ -1,7 +1,8 @@
 // pipck_rxparse.hpp -- device-side parse + verdict of one received IP packet
 // (pipck_rx_verify_device; see pipck_rxdev.hip for the design).  Included by
-// pipck_packedb.hip, whose k_packedb_rx calls rx_device_one at
-// each tile's end with the frame sum it has just streamed.
+// pipck_packedb.hip, whose k_packedb_rx calls rx_from_window at each tile's end
+// with the frame sum it has just streamed and the header window it captured
+// (rx_device_one reads the window from memory: tiles with a frame under 16 B).
 #pragma once
 #include "pipck_device.hpp"
 
@@ -64,21 +65,27 @@ __device__ __forceinline__ uint32_t range_sum(const uint8_t* p, const uint32_t (
 // One packet: p its first byte (any alignment), len its frame bytes, sall the
 // folded big-endian sum of the whole frame from pass 1.  Returns the ok bits
 // pipck_rx_verify gives the same bytes (rx_parse + k_rx_verify, pipck_rx.hip).
-__device__ inline uint32_t rx_device_one(const uint8_t* p, uint32_t len, uint32_t sall) {
-    if (len < 20) return 0;
-    // six aligned 16-byte chunks from the one holding byte 0, none past the one
-    // holding the frame's last byte (bytes after the frame in that chunk belong
-    // to the next packet and are never used: every range below ends <= len)
+// The packet's first six aligned 16-byte chunks (from the one holding byte 0),
+// none past the one holding its last byte.
+__device__ __forceinline__ void rx_window_global(const uint8_t* p, uint32_t len, uint32_t (&w)[24]) {
     // (global loads with a per-lane guard: a buffer resource is scalar, and one
     // per lane made the compiler loop over the wave's 64 packet addresses)
     const uint32_t h = (uint32_t)((uintptr_t)p & 15u);
     const u32x4* base = reinterpret_cast<const u32x4*>(p - h);
-    uint32_t w[24];
 #pragma unroll
     for (int c = 0; c < 6; c++) {
         const u32x4 v = 16u * c < h + len ? load_plain(base + c) : u32x4{0u, 0u, 0u, 0u};
         w[4 * c] = v.x, w[4 * c + 1] = v.y, w[4 * c + 2] = v.z, w[4 * c + 3] = v.w;
     }
+}
+
+// One packet whose window w (rx_window_global's chunks; chunks past the one
+// holding the last byte zero) is already in registers.
+__device__ inline uint32_t rx_from_window(const uint8_t* p, uint32_t len, uint32_t sall, const uint32_t (&w)[24]) {
+    if (len < 20) return 0;
+    const uint32_t h = (uint32_t)((uintptr_t)p & 15u);
+    // (bytes after the frame in its last chunk belong to the next packet and
+    // are never used: every range below ends <= len)
     // realign: a[k] = bytes [4k, 4k + 4) of the packet
     // (shifts by 2 and 1 words as masked blends: written as selects, the
     // compiler turned them into an indexed copy through scratch memory)
@@ -147,7 +154,14 @@ __device__ inline uint32_t rx_device_one(const uint8_t* p, uint32_t len, uint32_
         if (up == 0) return out | kOkL4;    // fragment, routing header: unchecked
         proto = nh;
         l4off = at;
-        le_pre = range_sum(p, a, 0, l4off);
+        if (l4off == 40) {  // no extension headers (the common case): the fixed header's ten words
+            uint32_t f = 0;
+#pragma unroll
+            for (int k = 0; k < 10; k++) f = dot_fold(a[k], f);
+            le_pre = f;
+        } else {
+            le_pre = range_sum(p, a, 0, l4off);
+        }
         uint32_t s = 0;
 #pragma unroll
         for (int k = 2; k < 10; k++) s = dot_fold(a[k], s);  // [8, 40)
@@ -159,7 +173,10 @@ __device__ inline uint32_t rx_device_one(const uint8_t* p, uint32_t len, uint32_
     if (proto != 6u && proto != 17u && !icmp) return out | kOkL4;  // no checksum this knows
     const uint32_t l4len = ip_end - l4off;
     if (l4len < (proto == 6u ? 20u : 8u)) return out;  // truncated: L4 bits clear
-    if (proto == 17u && v4 && !win_byte(a, l4off + 6) && !win_byte(a, l4off + 7)) return out | kOkL4;
+    if (proto == 17u && v4) {  // the UDP checksum field, bytes l4off + 6 and + 7 (static when IHL is 5)
+        const uint32_t f = l4off == 20 ? (a[6] >> 16) : (win_byte(a, l4off + 6) | win_byte(a, l4off + 7));
+        if (!f) return out | kOkL4;
+    }
     // S_l4 = S_all - S_pre - S_post, all big-endian relative to the packet start
     const uint32_t pre = bswap16(fold16(le_pre));
     const uint32_t post = ip_end < len ? bswap16(fold16(range_sum(p, a, ip_end, len))) : 0u;
@@ -173,6 +190,12 @@ __device__ inline uint32_t rx_device_one(const uint8_t* p, uint32_t len, uint32_
     const uint32_t P = proto + pseudo_addr + (l4len >> 16) + (l4len & 0xFFFFu);
     if (fold16(P + x) == 0xFFFFu) out |= kOkL4;
     return out;
+}
+
+__device__ inline uint32_t rx_device_one(const uint8_t* p, uint32_t len, uint32_t sall) {
+    uint32_t w[24];
+    rx_window_global(p, len, w);
+    return rx_from_window(p, len, sall, w);
 }
 
 }  // namespace pipck

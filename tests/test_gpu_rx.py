@@ -225,6 +225,12 @@ def test_rx_verify_device_edges(oracle):
     for (p, w), got in zip(cases, dev):
         if w is not None:
             assert got == w, (p[:48].hex(), got, w)
+    # a tile holding a frame under 16 bytes reads its headers from memory; the
+    # others take them from the stream (k_packedb_rx's capture): both, here
+    keep = [i for i, p in enumerate(frames) if len(p) >= 16]
+    arena, lens, tile_off = _device_batch([frames[i] for i in keep])
+    dev2 = engine.rx_verify_device(arena, lens, tile_off).cpu().numpy()
+    assert list(dev2) == [host[i] for i in keep]
 
 
 @pytest.mark.gpu
