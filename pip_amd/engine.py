@@ -357,6 +357,76 @@ def gen_packed_bytes(n: int, first: int, seed: int, hdr: int, device=None, lengt
     return arena, lens16, tile_off, lengths
 
 
+def gen_rx_frames(n: int, seed: int, checksummed: bool = True):
+    """Received-frame batch for pipck_rx_verify_device (bench and tests; synthetic):
+    n frames back to back, cfg4's Zipf L4 lengths (64-9,000 B) under an IPv4 (kinds
+    0, 1: TCP; 2: UDP) or IPv6 (kind 3: TCP) header, every other byte random.  With
+    `checksummed`, the TCP/UDP and IPv4 header checksum fields are filled in by this
+    engine's own batch kernels (pipck_checksum_ragged over the L4 segments with each
+    frame's pseudo-header, then over the 20-byte IPv4 headers), as a sender would,
+    so every frame verifies except UDP/IPv4 ones whose checksum came out 0x0000 (sent
+    as "no checksum", RFC 768).  Returns (arena, lens u16-in-int16, tile_off, kind,
+    start, l4_len) with start / l4_len int64 on the device."""
+    torch = _torch()
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    l4 = torch.empty(n, dtype=torch.int32, device="cuda")
+    call("pipck_gen_zipf_lengths", _ptr(l4), n, 0, cfg_seed(4), current_stream())
+    kind = torch.randint(0, 4, (n,), device="cuda", generator=g)
+    v6 = kind == 3
+    hl = torch.where(v6, 40, 20).to(torch.int64)
+    l4 = l4.to(torch.int64)
+    frame = l4 + hl
+    lens = frame.to(torch.int16)
+    tile_off = packed_bytes_index(lens)
+    total = int(tile_off[-1].item())
+    arena = torch.randint(0, 256, ((total + 16 + 127) // 128 * 128,), dtype=torch.uint8, device="cuda", generator=g)
+    start = torch.cumsum(frame, 0) - frame
+    proto = torch.where(kind == 2, 17, 6)
+
+    def put(col, val, mask):
+        idx = (start + col)[mask]
+        arena[idx] = (val[mask] if torch.is_tensor(val) else torch.full_like(idx, val)).to(torch.uint8)
+
+    v4 = ~v6
+    put(0, 0x45, v4)
+    put(2, frame >> 8, v4)
+    put(3, frame & 0xFF, v4)
+    put(6, 0, v4)  # not a fragment
+    put(7, 0, v4)
+    put(9, proto, v4)
+    put(0, 0x60, v6)
+    put(4, l4 >> 8, v6)
+    put(5, l4 & 0xFF, v6)
+    put(6, 6, v6)
+    if not checksummed:
+        return arena, lens, tile_off, kind, start, l4
+    field = start + hl + torch.where(proto == 6, 16, 6)  # th_sum / uh_sum
+    for k in (0, 1):
+        arena[field + k] = 0
+    put(10, 0, v4)
+    put(11, 0, v4)
+
+    def be_words(first, count):  # big-endian 16-bit words of [start + first, + 2 * count) summed
+        idx = start[:, None] + first + torch.arange(2 * count, device="cuda")
+        b = arena[idx].to(torch.int64)
+        return (b[:, 0::2] * 256 + b[:, 1::2]).sum(1)
+
+    pseudo = torch.where(v6, be_words(8, 16), be_words(12, 4)) + proto  # addresses + proto (pip_checksum.cpp:45-82)
+    flows = torch.arange(n, device="cuda", dtype=torch.int64)
+
+    def ragged(off, ln, ps):
+        desc = torch.stack([off, ln | (flows << 32)], 1)
+        return checksum_ragged(arena, desc, ps).to(torch.int64) & 0xFFFF
+
+    r = ragged(start + hl, l4, pseudo.to(torch.int32))
+    arena[field] = (r >> 8).to(torch.uint8)
+    arena[field + 1] = (r & 0xFF).to(torch.uint8)
+    ip = ragged(start, torch.full_like(l4, 20), None)
+    put(10, ip >> 8, v4)
+    put(11, ip & 0xFF, v4)
+    return arena, lens, tile_off, kind, start, l4
+
+
 def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, plain_loads: bool = False,
          flat: bool = True, nt_loads: bool = False, rows_per_task: int = 0, xcd_groups: bool = False,
          packed_tiles: bool = True, wide_blocks: bool = False,

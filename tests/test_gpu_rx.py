@@ -257,3 +257,42 @@ def test_rx_verify_device_bounded_by_the_arena(oracle):
     got = ok.cpu().numpy()
     assert (got[:64] == VERIFIED).all() and (got[64:] == 0).all()
     assert int(err.item()) & (1 << _lib.PIPCK_ERANGE)
+
+
+@pytest.mark.gpu
+def test_rx_verify_device_full_size():
+    """BASELINE scale (8M frames, cfg4's Zipf lengths, 8.5 GB): frames whose
+    TCP/UDP and IPv4 header checksums this engine's ragged kernel filled in
+    (engine.gen_rx_frames) all verify -- except UDP/IPv4 frames whose checksum
+    came out 0x0000, sent as "no checksum" and reported unchecked -- and one
+    flipped byte in 4,000 sampled frames fails exactly the checksum covering
+    it (a checksum-of-checksum property: two kernels, sizes the oracle cannot
+    reach)."""
+    import torch
+
+    from pip_amd import engine
+
+    n = 8 << 20
+    arena, lens, tile_off, kind, start, l4 = engine.gen_rx_frames(n, 77)
+    hl = torch.where(kind == 3, 40, 20)
+    field = start + hl + torch.where(kind == 2, 6, 16)
+    no_sum = (kind == 2) & (arena[field] == 0) & (arena[field + 1] == 0)
+    want = torch.full((n,), VERIFIED, dtype=torch.uint8, device="cuda")
+    want[no_sum] = UNCHECKED
+    ok = engine.rx_verify_device(arena, lens, tile_off)
+    assert torch.equal(ok, want), int((ok != want).sum().item())
+    # one byte flipped: an L4 payload byte (not the checksum field) or an IPv4 TTL
+    g = torch.Generator(device="cuda").manual_seed(5)
+    pick = torch.randperm(n, device="cuda", generator=g)[:4000]
+    pick = pick[~no_sum[pick]]
+    half = pick.numel() // 2
+    l4_pick, ip_pick = pick[:half], pick[half:]
+    ip_pick = ip_pick[kind[ip_pick] != 3]
+    where = start[l4_pick] + hl[l4_pick] + 18 + (torch.rand(half, device="cuda", generator=g) *
+                                                (l4[l4_pick] - 18).to(torch.float32)).to(torch.int64)
+    arena[where] ^= 0x10
+    arena[start[ip_pick] + 8] ^= 0x01
+    want[l4_pick] = IP_OK | L4_CHECKED
+    want[ip_pick] = VERIFIED & ~IP_OK
+    ok = engine.rx_verify_device(arena, lens, tile_off)
+    assert torch.equal(ok, want), int((ok != want).sum().item())
