@@ -408,6 +408,16 @@ int pipck_rx_verify(pipck_rxq* q, const void* const* pkts, const uint32_t* lens,
  * boundary after the last frame.  Bounded as pipck_checksum_packed_bytes_n: a tile
  * reaching past arena_bytes is not read, its packets get 0 and d_err
  * (optional) gets (1 << PIPCK_ERANGE).  Asynchronous. */
+/* The same for received frames back to back in HOST memory (a receive buffer
+ * read in order, a capture file's records): chunks of ~64 MiB go H2D by DMA
+ * with their u16 lengths, pipck_rx_verify_device judges them, the verdicts
+ * come back; double-buffered over the context's two streams, PCIe-bound at
+ * every frame size (pipck_rx_verify reads each packet in place with a wave of
+ * its own: better for scattered packets, slower for small ones).  h_frames
+ * pinned (pipck_host_alloc) for full rate; pageable works.  Synchronous;
+ * *n_verified (optional) = frames with ok == PIPCK_RX_VERIFIED. */
+int pipck_host_rx_verify_packed(pipck_ctx* ctx, const void* h_frames, const uint16_t* h_lens, uint64_t n_frames,
+                                uint8_t* h_ok, uint64_t* n_verified);
 int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                            const uint64_t* d_tile_off, uint64_t n_packets, uint8_t* d_ok, uint32_t* d_err,
                            void* stream);

@@ -741,6 +741,58 @@ int pipck_host_unregister(void* p) {
     return PIPCK_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Byte-packed host batches (packet i's h_lens[i] bytes right after packet
+// i-1's): chunks of whole packets, ~64 MiB of bytes (at most 1M packets) each,
+// double-buffered over the context's two streams -- H2D of the chunk's bytes
+// and lengths, its tile index (pipck_packed_bytes_index), then work(b, first,
+// m, stream) launches the chunk's kernel and its D2H.  Waits for both streams.
+// The caller holds c->mu and the device.
+template <typename Work>
+int host_packed_chunks(pipck_ctx* c, const void* h_arena, const uint16_t* h_lens, uint64_t n, Work&& work) {
+    constexpr uint64_t kTarget = 64ull << 20, kMaxPkts = 1ull << 20;
+    int rc;
+    if ((rc = reserve_chunks(c, (size_t)(kTarget + 65536 + 256), kMaxPkts))) return rc;  // overshoot < one packet
+    if (kMaxPkts > c->packed_cap) {
+        for (int i = 0; i < 2; i++) {
+            if (c->d_lens[i]) PIPCK_HIP(hipFree(c->d_lens[i]));
+            if (c->d_tile_off[i]) PIPCK_HIP(hipFree(c->d_tile_off[i]));
+            c->d_lens[i] = nullptr;
+            c->d_tile_off[i] = nullptr;
+        }
+        c->packed_cap = 0;
+        for (int i = 0; i < 2; i++) {
+            PIPCK_HIP(hipMalloc((void**)&c->d_lens[i], kMaxPkts * sizeof(uint16_t)));
+            PIPCK_HIP(hipMalloc((void**)&c->d_tile_off[i], (kMaxPkts / 64 + 2) * sizeof(uint64_t)));
+        }
+        c->packed_cap = kMaxPkts;
+    }
+    const uint8_t* src = (const uint8_t*)h_arena;
+    uint64_t first = 0, off = 0;
+    for (uint64_t k = 0; first < n; k++) {
+        uint64_t m = 0, bytes = 0;
+        while (first + m < n && m < kMaxPkts && bytes < kTarget) bytes += h_lens[first + m++];
+        const int b = (int)(k & 1);
+        hipStream_t s = c->stream[b];
+        if (bytes) PIPCK_HIP(hipMemcpyAsync(c->d_chunk[b], src + off, (size_t)bytes, hipMemcpyHostToDevice, s));
+        PIPCK_HIP(hipMemcpyAsync(c->d_lens[b], h_lens + first, m * sizeof(uint16_t), hipMemcpyHostToDevice, s));
+        if ((rc = pipck_packed_bytes_index(c->d_lens[b], m, c->d_tile_off[b], s))) return rc;
+        if ((rc = work(b, first, m, s))) return rc;
+        first += m;
+        off += bytes;
+    }
+    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
+    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
+    return PIPCK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 void* pipck_host_alloc(size_t bytes) {
     // coherent (fine-grained): kernels may read it in place (zero-copy TX
     // segments), and no device cache may keep bytes the host rewrites later
@@ -779,45 +831,38 @@ int pipck_host_checksum_packed_bytes(pipck_ctx* c, const void* h_arena, const ui
     const uint32_t* d_pseudo = nullptr;
     int rc = upload_flows(c, family, h_flows, n_flows, &d_pseudo);
     if (rc) return rc;
-    // Chunks of whole packets, ~64 MiB of bytes (at most kMaxPkts packets) each,
-    // double-buffered over the context's two streams: H2D of the chunk's bytes
-    // and lengths, its tile index (pipck_packed_bytes_index), k_packedb bounded
-    // by the chunk buffer, D2H of the results.
-    constexpr uint64_t kTarget = 64ull << 20, kMaxPkts = 1ull << 20;
-    if ((rc = reserve_chunks(c, (size_t)(kTarget + 65536 + 256), kMaxPkts))) return rc;  // overshoot < one packet
-    if (kMaxPkts > c->packed_cap) {
-        for (int i = 0; i < 2; i++) {
-            if (c->d_lens[i]) PIPCK_HIP(hipFree(c->d_lens[i]));
-            if (c->d_tile_off[i]) PIPCK_HIP(hipFree(c->d_tile_off[i]));
-            c->d_lens[i] = nullptr;
-            c->d_tile_off[i] = nullptr;
-        }
-        c->packed_cap = 0;
-        for (int i = 0; i < 2; i++) {
-            PIPCK_HIP(hipMalloc((void**)&c->d_lens[i], kMaxPkts * sizeof(uint16_t)));
-            PIPCK_HIP(hipMalloc((void**)&c->d_tile_off[i], (kMaxPkts / 64 + 2) * sizeof(uint64_t)));
-        }
-        c->packed_cap = kMaxPkts;
-    }
-    const uint8_t* src = (const uint8_t*)h_arena;
-    uint64_t first = 0, off = 0;
-    for (uint64_t k = 0; first < n; k++) {
-        uint64_t m = 0, bytes = 0;
-        while (first + m < n && m < kMaxPkts && bytes < kTarget) bytes += h_lens[first + m++];
-        const int b = (int)(k & 1);
-        hipStream_t s = c->stream[b];
-        if (bytes) PIPCK_HIP(hipMemcpyAsync(c->d_chunk[b], src + off, (size_t)bytes, hipMemcpyHostToDevice, s));
-        PIPCK_HIP(hipMemcpyAsync(c->d_lens[b], h_lens + first, m * sizeof(uint16_t), hipMemcpyHostToDevice, s));
-        if ((rc = pipck_packed_bytes_index(c->d_lens[b], m, c->d_tile_off[b], s))) return rc;
-        rc = pipck_checksum_packed_bytes_n(c->d_chunk[b], c->chunk_cap, c->d_lens[b], c->d_tile_off[b], m, d_pseudo,
-                                           n_flows, nullptr, flow_origin + first, c->d_out[b], nullptr, s);
-        if (rc) return rc;
+    return host_packed_chunks(c, h_arena, h_lens, n, [&](int b, uint64_t first, uint64_t m, hipStream_t s) {
+        int r = pipck_checksum_packed_bytes_n(c->d_chunk[b], c->chunk_cap, c->d_lens[b], c->d_tile_off[b], m,
+                                              d_pseudo, n_flows, nullptr, flow_origin + first, c->d_out[b], nullptr, s);
+        if (r) return r;
         PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
-        first += m;
-        off += bytes;
+        return PIPCK_OK;
+    });
+}
+
+int pipck_host_rx_verify_packed(pipck_ctx* c, const void* h_frames, const uint16_t* h_lens, uint64_t n, uint8_t* h_ok,
+                                uint64_t* n_verified) {
+    if (n_verified) *n_verified = 0;
+    if (!c || (n && (!h_frames || !h_lens || !h_ok))) {
+        set_error("pipck_host_rx_verify_packed: bad argument");
+        return PIPCK_EINVAL;
     }
-    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
-    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
+    if (!n) return PIPCK_OK;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    int rc = host_packed_chunks(c, h_frames, h_lens, n, [&](int b, uint64_t first, uint64_t m, hipStream_t s) {
+        uint8_t* d_ok = reinterpret_cast<uint8_t*>(c->d_out[b]);  // u16 per packet: room for the u8 verdicts
+        int r = pipck_rx_verify_device(c->d_chunk[b], c->chunk_cap, c->d_lens[b], c->d_tile_off[b], m, d_ok, nullptr, s);
+        if (r) return r;
+        PIPCK_HIP(hipMemcpyAsync(h_ok + first, d_ok, (size_t)m, hipMemcpyDeviceToHost, s));
+        return PIPCK_OK;
+    });
+    if (rc) return rc;
+    if (n_verified) {
+        uint64_t good = 0;
+        for (uint64_t i = 0; i < n; i++) good += h_ok[i] == PIPCK_RX_VERIFIED;
+        *n_verified = good;
+    }
     return PIPCK_OK;
 }
 

@@ -296,3 +296,59 @@ def test_rx_verify_device_full_size():
     want[ip_pick] = VERIFIED & ~IP_OK
     ok = engine.rx_verify_device(arena, lens, tile_off)
     assert torch.equal(ok, want), int((ok != want).sum().item())
+
+
+@pytest.mark.gpu
+def test_host_rx_verify_packed_equals_rx_verify(oracle):
+    """pipck_host_rx_verify_packed (frames back to back in host memory, DMA'd
+    in chunks and judged by pipck_rx_verify_device) gives pipck_rx_verify's
+    bits: the 5,000-packet batch with damage and padding (several 64-MiB
+    chunks when repeated), from pinned and from pageable memory, plus the edge
+    frames (empty, short: the lane-per-segment tiles)."""
+    from pip_amd import _lib
+
+    rng = random.Random(404)
+    frames, want = [], []
+    for k in range(5000):
+        fam = rng.choice([4, 6])
+        proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
+        l4len = rng.randint(8000, 9000) if k % 20 == 0 else rng.randint(20, 1500)
+        p = bytearray(_rx_packet(oracle, rng, fam, proto, l4len, k + 1))
+        checked = not (fam == 4 and proto == 17 and (k + 1) % 7 == 0)
+        w = VERIFIED if checked else UNCHECKED
+        hl = 20 if fam == 4 else 40
+        if k % 3 == 1 and checked:
+            i = rng.randrange(hl + 18, len(p)) if len(p) > hl + 18 else hl
+            p[i] ^= 0x20
+            w = IP_OK | L4_CHECKED
+        frames.append(bytes(p) + rng.randbytes(rng.choice([0, 5])))
+        want.append(w)
+    frames = frames * 15  # ~110 MB: more than one 64-MiB chunk
+    want = want * 15
+    frames += [b"", bytes(10), _rx_packet(oracle, rng, 4, 1, 8, 9)]
+    want += [0, 0, VERIFIED]
+    lib = _lib.load()
+    blob = b"".join(frames)
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    ctx = C.c_void_p()
+    assert lib.pipck_ctx_create(-1, C.byref(ctx)) == 0
+    try:
+        for pinned in (True, False):
+            if pinned:
+                p = lib.pipck_host_alloc(len(blob))
+                C.memmove(p, blob, len(blob))
+                base = p
+            else:
+                buf = np.frombuffer(blob, dtype=np.uint8).copy()
+                base = buf.ctypes.data
+            ok = np.full(len(frames), 0xEE, dtype=np.uint8)
+            good = C.c_uint64(99)
+            rc = lib.pipck_host_rx_verify_packed(ctx, base, lens.ctypes.data, len(frames), ok.ctypes.data,
+                                                 C.byref(good))
+            assert rc == 0, lib.pipck_last_error()
+            assert list(ok) == want, pinned
+            assert good.value == int((ok == VERIFIED).sum())
+            if pinned:
+                assert lib.pipck_host_free(C.c_void_p(p)) == 0
+    finally:
+        lib.pipck_ctx_destroy(ctx)

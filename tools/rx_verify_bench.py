@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--sizes", default="1500,9000")
     ap.add_argument("--batches", default="1024,16384,65536")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--packed", action="store_true",
+                    help="also time pipck_host_rx_verify_packed on the same frames (they lie back to back)")
     a = ap.parse_args()
     shim = C.CDLL(str(_lib.LIBSHIM))
     fn = shim.pip_checksum_amd_verify_packets
@@ -67,6 +69,27 @@ def main():
                                   "ms_per_call": round(t * 1e3, 4), "gib_per_s": round(total / t / 2**30, 3),
                                   "mpkt_per_s": round(n / t / 1e6, 3), "verified": int((ok == 7).sum()),
                                   "l4_checked": int(((ok & 4) != 0).sum())}), flush=True)
+                if a.packed:  # the same frames, back to back: one DMA stream per chunk, verdicts on the device
+                    ctx = C.c_void_p()
+                    assert lib.pipck_ctx_create(-1, C.byref(ctx)) == 0
+                    l16 = np.full(n, size, dtype=np.uint16)
+                    ok2 = np.zeros(n, dtype=np.uint8)
+                    good = C.c_uint64()
+                    hp = lib.pipck_host_rx_verify_packed
+                    assert hp(ctx, base, l16.ctypes.data, n, ok2.ctypes.data, C.byref(good)) == 0  # warm
+                    ts = []
+                    for _ in range(a.reps):
+                        t0 = time.perf_counter()
+                        hp(ctx, base, l16.ctypes.data, n, ok2.ctypes.data, C.byref(good))
+                        ts.append(time.perf_counter() - t0)
+                    t2 = statistics.median(ts)
+                    assert np.array_equal(ok, ok2)
+                    print(json.dumps({"tool": "rx_verify_bench", "api": "pipck_host_rx_verify_packed",
+                                      "packet_bytes": size, "batch": n, "memory": mem,
+                                      "ms_per_call": round(t2 * 1e3, 4), "gib_per_s": round(total / t2 / 2**30, 3),
+                                      "mpkt_per_s": round(n / t2 / 1e6, 3), "verified": int(good.value),
+                                      "verdicts_equal_drop_in": True}), flush=True)
+                    lib.pipck_ctx_destroy(ctx)
                 del pk, buf
                 if mem == "pinned":
                     lib.pipck_host_free(C.c_void_p(p))
