@@ -115,8 +115,10 @@ bool pip_checksum_amd_capturing();
 // malformed packet (lengths that do not fit, a truncated TCP/UDP/ICMP header,
 // not IPv4/IPv6) gets no L4 bits, or 0.  IPv6 hop-by-hop / destination-options
 // headers and atomic fragments are walked to the upper layer.  Packets in
-// pinned memory are read in place; the call returns when every result is
-// known.  Returns the number of packets with ok == PIP_RX_VERIFIED.  Uses its
+// pinned memory are read in place; packets that lie back to back in one buffer
+// (pkts[i + 1] == pkts[i] + lens[i]) go to the GPU in one DMA per chunk
+// (pipck_host_rx_verify_packed) -- same bits; the call returns when every
+// result is known.  Returns the number of packets with ok == PIP_RX_VERIFIED.  Uses its
 // own queue: pip's deferred TX batch is not touched.
 #define PIP_RX_IP_OK 1u
 #define PIP_RX_L4_OK 2u

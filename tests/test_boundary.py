@@ -184,7 +184,9 @@ def test_pip_udp_tx_path_matches_pip(family, length):
 
 
 def _verify(packets):
-    """pip_checksum_amd_verify_packets (the drop-in's RX batch verifier) over Python bytes."""
+    """pip_checksum_amd_verify_packets (the drop-in's RX batch verifier) over Python bytes,
+    once with every packet in its own buffer and once with the packets back to back in
+    one buffer (the drop-in then takes the chunked-DMA path): the same bits both ways."""
     import ctypes as C
 
     import numpy as np
@@ -195,12 +197,18 @@ def _verify(packets):
     fn = lib.pip_checksum_amd_verify_packets
     fn.restype = C.c_uint32
     fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p]
+    lens = (C.c_uint32 * len(packets))(*[len(p) for p in packets])
     bufs = [C.create_string_buffer(bytes(p), max(len(p), 1)) for p in packets]
     ptrs = (C.c_void_p * len(packets))(*[C.cast(b, C.c_void_p) for b in bufs])
-    lens = (C.c_uint32 * len(packets))(*[len(p) for p in packets])
     ok = np.zeros(len(packets), dtype=np.uint8)
     good = fn(ptrs, lens, len(packets), ok.ctypes.data)
     assert good == int((ok == VERIFIED).sum())
+    blob = C.create_string_buffer(b"".join(bytes(p) for p in packets), max(sum(len(p) for p in packets), 1))
+    base, offs = C.cast(blob, C.c_void_p).value, np.cumsum([0] + [len(p) for p in packets[:-1]])
+    ptrs2 = (C.c_void_p * len(packets))(*[base + int(o) for o in offs])
+    ok2 = np.zeros(len(packets), dtype=np.uint8)
+    good2 = fn(ptrs2, lens, len(packets), ok2.ctypes.data)
+    assert good2 == good and np.array_equal(ok2, ok), np.nonzero(ok2 != ok)[0][:5]
     return ok
 
 
