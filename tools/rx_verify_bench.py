@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""RX batch verification rate (pip_checksum_amd_verify_packets, the drop-in's
-SURVEY 8 f2 helper) from host memory: N TCP/IPv4 packets of a given size,
+"""RX batch verification rate (pipck_rx_verify, the per-packet verifier behind the
+drop-in's pip_checksum_amd_verify_packets) from host memory: N TCP/IPv4 packets of a given size,
 heap (copied into the queue's staging) or pinned (pipck_host_alloc: read in
 place), one call per batch.  One JSON line per (size, batch, memory).
 
@@ -31,11 +31,18 @@ def main():
     ap.add_argument("--packed", action="store_true",
                     help="also time pipck_host_rx_verify_packed on the same frames (they lie back to back)")
     a = ap.parse_args()
-    shim = C.CDLL(str(_lib.LIBSHIM))
-    fn = shim.pip_checksum_amd_verify_packets
-    fn.restype = C.c_uint32
-    fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_void_p]
     lib = _lib.load()
+    # the per-packet verifier through its C ABI (pipck_rx_verify): the drop-in's
+    # pip_checksum_amd_verify_packets now sends batches that lie back to back in
+    # one buffer -- as here -- to pipck_host_rx_verify_packed instead
+    rxq = C.c_void_p()
+    assert lib.pipck_rxq_create(None, C.byref(rxq)) == 0
+
+    def fn(ptrs, lens, n, ok_ptr):
+        good = C.c_uint64()
+        assert lib.pipck_rx_verify(rxq, ptrs, lens, n, ok_ptr, C.byref(good)) == 0
+        return good.value
+
     rng = np.random.default_rng(3)
     for size in (int(x) for x in a.sizes.split(",")):
         for n in (int(x) for x in a.batches.split(",")):
