@@ -153,6 +153,37 @@ def test_tx_bench_on_pips_own_build_reports_resend_ages():
             "write", "ack input", "syn -> syn-ack", "handshake ack", "flush")
         assert d["stale_clock_resends"] >= 0 and (d["stale_clock_resends"] == 0) == (d["max_resend_age_ms"] == 0)
         assert d["packets"] > (64 << 20) // 1460
+    # the ip_id-independent digest (stack_tx_bench.cpp digest_noid) of two runs of
+    # pip's own build agrees even when pip's timer raced in one of them
+    runs = []
+    for _ in range(2):
+        r = subprocess.run([str(ref_bin), "--family", "4", "--mss", "1460", "--bytes", str(16 << 20), "--write",
+                            str(1 << 20), "--conns", "2", "--verify"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert runs[0]["digest_noid"] == runs[1]["digest_noid"] and runs[0]["packets"] == runs[1]["packets"]
+    if runs[0]["stale_clock_resends"] == runs[1]["stale_clock_resends"] == 0:
+        assert runs[0]["digest"] == runs[1]["digest"]
+
+
+def test_ip_id_normalisation_keeps_header_validity():
+    """_without_ip_id (the stack replay's comparison under pip's timer race):
+    ip_id and ip_sum give way to the header's validity, everything else stays."""
+    import struct
+
+    def v4(ident, good):
+        h = bytearray(struct.pack(">BBHHHBBH4s4s", 0x45, 0, 28, ident, 0x4000, 64, 17, 0, b"\x0a\0\0\x01",
+                                  b"\x0a\0\0\x02"))
+        s = sum(h[i] << 8 | h[i + 1] for i in range(0, 20, 2))
+        while s >> 16:
+            s = (s & 0xFFFF) + (s >> 16)
+        h[10:12] = struct.pack(">H", (~s & 0xFFFF) ^ (0 if good else 1))
+        return (bytes(h) + b"\x01\x02\x03\x04\x05\x06\x07\x08").hex()
+
+    assert _without_ip_id(v4(1, True)) == _without_ip_id(v4(2, True))
+    assert _without_ip_id(v4(1, True)) != _without_ip_id(v4(1, False))
+    six = "60000000000811400000000000000000000000000000000100000000000000000000000000000002" + "00" * 8
+    assert _without_ip_id(six) == six and _without_ip_id("PACKETS 3") == "PACKETS 3"
 
 
 @pytest.mark.gpu
