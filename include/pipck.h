@@ -408,6 +408,13 @@ int pipck_rx_verify(pipck_rxq* q, const void* const* pkts, const uint32_t* lens,
  * boundary after the last frame.  Bounded as pipck_checksum_packed_bytes_n: a tile
  * reaching past arena_bytes is not read, its packets get 0 and d_err
  * (optional) gets (1 << PIPCK_ERANGE).  Asynchronous. */
+/* The same for frames in the fixed-size slots of a receive ring in DEVICE
+ * memory: frame i (d_lens[i] <= slot_stride bytes) at d_arena + i *
+ * slot_stride, the rest of each slot unused and never read.  d_arena 16-byte
+ * aligned; slot_stride a multiple of 16 from 1,024 to 65,536 (PIPCK_EINVAL
+ * otherwise).  One kernel on `stream`; d_ok[i] as pipck_rx_verify_device. */
+int pipck_rx_verify_ring(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n_slots,
+                         uint8_t* d_ok, void* stream);
 /* The same for received frames back to back in HOST memory (a receive buffer
  * read in order, a capture file's records): chunks of ~64 MiB go H2D by DMA
  * with their u16 lengths, pipck_rx_verify_device judges them, the verdicts

@@ -102,6 +102,7 @@ SIGNATURES = {
     "pipck_rx_verify": (_i32, [_p, _p, _p, _u64, _p, C.POINTER(_u64)]),
     "pipck_rx_verify_device": (_i32, [_p, _u64, _p, _p, _u64, _p, _p, _p]),
     "pipck_host_rx_verify_packed": (_i32, [_p, _p, _p, _u64, _p, C.POINTER(_u64)]),
+    "pipck_rx_verify_ring": (_i32, [_p, _u64, _p, _u64, _p, _p]),
 }
 
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only

@@ -32,8 +32,158 @@
 // apart from T = k x 0xFFFF, so the kernel checks the message for a non-zero
 // byte (its first 8 bytes from registers, the rest only if those are zero).
 #include "pipck_common.hpp"
+#include "pipck_rxparse.hpp"
+
+#include <algorithm>
+
+namespace pipck {
+
+// ---- frames in fixed-size slots (a receive ring: slot i at arena + i * stride,
+// lens[i] bytes of frame in it, the rest of the slot unused) -----------------
+// k_ring_rx streams the slots like k_flat_coop (pipck_coop.hip): a block task
+// of K whole slots, its four waves on interleaved 1 KiB rows, a ring of U rows
+// per wave, one LDS partial per lane per slot.  Unlike k_flat_coop each lane's
+// load is predicated on the chunk lying inside its slot's frame (the slot's
+// length from LDS), so the unused part of a slot is never read -- a sparse ring
+// (short frames in jumbo slots) costs its frame bytes, not its slot bytes.  Each
+// slot's first six chunks (its header window; slots are 16-byte aligned) are
+// copied to LDS on the way, and at the task's end thread j judges slot j with
+// rx_from_window (pipck_rxparse.hpp) from the frame's sum and that window.
+constexpr int kRingU = 24;
+
+__host__ __device__ constexpr uint32_t ring_pitch(uint32_t k) { return k | 1u; }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_ring_rx(
+    const uint8_t* __restrict__ arena, uint32_t cpp, const uint16_t* __restrict__ lens, uint64_t n, uint32_t K,
+    uint8_t* __restrict__ ok) {
+    extern __shared__ uint32_t s_ring[];  // part[64][pitch] | len[K] | hdr[6][K] (u32x4), launch_ring_rx sizes it
+    const uint32_t pitch = ring_pitch(K);
+    uint32_t* s_part = s_ring;
+    uint32_t* s_len = s_part + 64u * pitch;
+    u32x4* hdr = reinterpret_cast<u32x4*>(s_len + ((K + 3u) & ~3u));
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t p0 = (uint64_t)blockIdx.x * K;
+    const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)K, n - p0);
+    const uint32_t rows = (np * cpp + 63u) >> 6;
+    for (uint32_t i = threadIdx.x; i < 64u * pitch; i += 256) s_part[i] = 0;
+    for (uint32_t i = threadIdx.x; i < K; i += 256) s_len[i] = i < np ? (uint32_t)lens[p0 + i] : 0u;
+    __syncthreads();
+    const buf_t tb = buf_rsrc(arena + p0 * cpp * 16u, np * cpp * 16u);
+    uint32_t* part = s_part + lane * pitch;
+    // this wave's rows w, w+4, ...: lane 0's slot and chunk-in-slot, advanced by
+    // 256 chunks (q slots + rm chunks) per row, for the row consumed and for the
+    // row loaded U rows ahead
+    const uint32_t q = 256u / cpp, rm = 256u % cpp;
+    uint32_t pkt = (64u * w) / cpp, k0 = (64u * w) % cpp;
+    uint32_t lpkt = pkt, lk0 = k0;
+    const uint32_t my_rows = rows > w ? (rows - w + 3) >> 2 : 0u;
+    auto step = [&](uint32_t& pk, uint32_t& kk) {
+        kk += rm;
+        pk += q;
+        if (kk >= cpp) {
+            kk -= cpp;
+            pk++;
+        }
+    };
+    // the load of row j of this wave, only where the chunk lies in its frame
+    auto load = [&](uint32_t j) -> u32x4 {
+        uint32_t k = lk0 + (uint32_t)lane, pk = lpkt;
+        if (k >= cpp) {
+            k -= cpp;
+            pk++;
+        }
+        const uint32_t L = pk < np ? s_len[pk] : 0u;
+        // past the frame: an offset beyond the resource, which reads zeros with
+        // no memory request (a predicated load would make every row wait vmcnt(0))
+        return buf_load<true>(tb, 16u * k < L ? ((w + 4u * j) * 64u + (uint32_t)lane) * 16u : 0xFFFFFFF0u);
+    };
+    u32x4 v[kRingU];
+#pragma unroll
+    for (int u = 0; u < kRingU; u++) {
+        v[u] = load((uint32_t)u);
+        step(lpkt, lk0);
+    }
+    for (uint32_t j0 = 0; j0 < my_rows; j0 += kRingU) {
+#pragma unroll
+        for (int u = 0; u < kRingU; u++) {
+            const uint32_t j = j0 + u;
+            if (j < my_rows) {  // wave-uniform
+                uint32_t k = k0 + (uint32_t)lane, pk = pkt;
+                if (k >= cpp) {
+                    k -= cpp;
+                    pk++;
+                }
+                const uint32_t L = pk < np ? s_len[pk] : 0u;
+                u32x4 x = v[u];
+                if (16u * k + 16u > L) x = 16u * k < L ? mask_tail(x, (int)(L - 16u * k)) : u32x4{0u, 0u, 0u, 0u};
+                if (pk < np) {
+                    atomicAdd(&part[pk], dot4(x, 0u));
+                    if (k < 6u) hdr[k * K + pk] = x;  // the slot's header window (bytes past the frame zero)
+                }
+                step(pkt, k0);
+            }
+            v[u] = load(j + kRingU);  // past the task: the resource's range check reads nothing
+            step(lpkt, lk0);
+        }
+    }
+    __syncthreads();
+    const uint32_t i = threadIdx.x;
+    if (i < np) {
+        uint32_t s = 0;
+#pragma unroll 16
+        for (int l = 0; l < 64; l++) s += s_part[l * pitch + i];
+        const uint32_t L = s_len[i];
+        const uint32_t F = bswap16(fold16(s));  // slots start 16-byte aligned: even address
+        uint32_t hw[24];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {  // chunks past the frame were never captured: zero
+            const u32x4 x = 16u * k < L ? hdr[k * K + i] : u32x4{0u, 0u, 0u, 0u};
+            hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
+        }
+        const uint8_t* pkp = arena + (p0 + i) * cpp * 16u;
+        store_result8(buf_rsrc(ok + p0, np), i, rx_from_window(pkp, L, F, hw));
+    }
+}
+
+int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
+                   hipStream_t s) {
+    if (n == 0) return PIPCK_OK;
+    if (!d_arena || !d_lens || !d_ok) {
+        set_error("pipck_rx_verify_ring: null pointer");
+        return PIPCK_EINVAL;
+    }
+    if ((uintptr_t)d_arena % 16 || stride % 16 || stride < 1024 || stride > 65536) {
+        set_error("pipck_rx_verify_ring: the arena must be 16-byte aligned and the slot stride a multiple of 16 "
+                  "bytes from 1 KiB to 64 KiB");
+        return PIPCK_EINVAL;
+    }
+    const uint32_t cpp = (uint32_t)(stride / 16);
+    // K slots per block task: ~4 waves x 48 rows (x 64 for jumbo slots), a
+    // multiple of 8, at most 256 (one slot per thread at the end) -- k_flat_coop's
+    uint32_t K = (4u * (cpp >= 256 ? 64u : 48u) * 64u) / cpp;
+    K = std::max<uint32_t>(8u, std::min<uint32_t>(256u, K / 8u * 8u));
+    if ((uint64_t)K * stride >= (1ull << 31)) return PIPCK_EINVAL;
+    const uint64_t blocks = (n + K - 1) / K;
+    if (blocks > 0x7FFFFFFFull) {
+        set_error("pipck_rx_verify_ring: too many slots for one launch");
+        return PIPCK_ERANGE;
+    }
+    const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
+    PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
+                 d_ok);
+    PIPCK_LAUNCHED("k_ring_rx");
+    return PIPCK_OK;
+}
+
+}  // namespace pipck
 
 extern "C" {
+
+int pipck_rx_verify_ring(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n,
+                         uint8_t* d_ok, void* stream) {
+    return pipck::launch_ring_rx(d_arena, slot_stride, d_lens, n, d_ok, pipck::as_stream(stream));
+}
 
 int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                            const uint64_t* d_tile_off, uint64_t n, uint8_t* d_ok, uint32_t* d_err, void* stream) {

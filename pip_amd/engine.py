@@ -234,6 +234,19 @@ def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None
     return ok
 
 
+def rx_verify_ring(ring, stride: int, lens, n: int | None = None, ok=None):
+    """Received frames in the fixed-size slots of a device ring (pipck_rx_verify_ring): the
+    PIPCK_RX_* bits per slot (uint8)."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if n * stride > _nbytes(ring):
+        raise ValueError("ring smaller than n * stride")
+    if ok is None:
+        ok = torch.empty(n, dtype=torch.uint8, device=ring.device)
+    call("pipck_rx_verify_ring", _ptr(ring), stride, _ptr(lens), n, _ptr(ok), current_stream(ring.device))
+    return ok
+
+
 def rx_verify_device(arena, lens, tile_off, n: int | None = None, ok=None, err=None):
     """Received IP packets in device memory, byte-packed (pipck_rx_verify_device): the
     PIPCK_RX_* bits per packet (uint8), as pipck_rx_verify gives for the same bytes in
@@ -357,9 +370,32 @@ def gen_packed_bytes(n: int, first: int, seed: int, hdr: int, device=None, lengt
     return arena, lens16, tile_off, lengths
 
 
-def gen_rx_frames(n: int, seed: int, checksummed: bool = True):
+def gen_rx_ring(n: int, seed: int, stride: int, l4_len: int = 0):
+    """gen_rx_frames laid out in the fixed-size slots of a receive ring: frame i at
+    ring[i * stride], the rest of each slot zero (pipck_rx_verify_ring's layout).
+    l4_len > 0: every frame's L4 length (a dense ring), else cfg4's Zipf lengths.
+    Returns (ring, lens u16-in-int16, kind)."""
+    torch = _torch()
+    arena, lens, _, kind, start, l4 = gen_rx_frames(n, seed, l4_len=l4_len)
+    ln = lens.to(torch.int64) & 0xFFFF
+    if int(ln.max().item()) > stride:
+        raise ValueError("a frame is longer than the slot stride")
+    ring = torch.zeros(n * stride, dtype=torch.uint8, device=arena.device)
+    step = 1 << 16  # frames per copy pass (bounded index tensors)
+    for f0 in range(0, n, step):
+        lc, sc = ln[f0:f0 + step], start[f0:f0 + step]
+        m = lc.numel()
+        frame = torch.repeat_interleave(torch.arange(m, device=arena.device), lc)
+        excl = torch.cumsum(lc, 0) - lc
+        within = torch.arange(frame.numel(), device=arena.device) - excl[frame]
+        ring[(f0 + frame) * stride + within] = arena[sc[frame] + within]
+    return ring, lens, kind
+
+
+def gen_rx_frames(n: int, seed: int, checksummed: bool = True, l4_len: int = 0):
     """Received-frame batch for pipck_rx_verify_device (bench and tests; synthetic):
-    n frames back to back, cfg4's Zipf L4 lengths (64-9,000 B) under an IPv4 (kinds
+    n frames back to back, cfg4's Zipf L4 lengths (64-9,000 B; l4_len > 0: all that
+    length) under an IPv4 (kinds
     0, 1: TCP; 2: UDP) or IPv6 (kind 3: TCP) header, every other byte random.  With
     `checksummed`, the TCP/UDP and IPv4 header checksum fields are filled in by this
     engine's own batch kernels (pipck_checksum_ragged over the L4 segments with each
@@ -370,7 +406,10 @@ def gen_rx_frames(n: int, seed: int, checksummed: bool = True):
     torch = _torch()
     g = torch.Generator(device="cuda").manual_seed(seed)
     l4 = torch.empty(n, dtype=torch.int32, device="cuda")
-    call("pipck_gen_zipf_lengths", _ptr(l4), n, 0, cfg_seed(4), current_stream())
+    if l4_len:
+        l4.fill_(l4_len)
+    else:
+        call("pipck_gen_zipf_lengths", _ptr(l4), n, 0, cfg_seed(4), current_stream())
     kind = torch.randint(0, 4, (n,), device="cuda", generator=g)
     v6 = kind == 3
     hl = torch.where(v6, 40, 20).to(torch.int64)

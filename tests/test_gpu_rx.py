@@ -402,3 +402,68 @@ def test_rx_device_parser_fuzz_equals_host_parser(oracle):
     bad = np.nonzero(dev2 != host[keep])[0]
     assert bad.size == 0, [(int(keep[i]), frames[keep[i]][:64].hex(), int(host[keep[i]]), int(dev2[i])) for i in bad[:3]]
     assert len(set(host.tolist())) >= 6  # the fuzz reaches many verdicts
+
+
+def _ring(frames, stride):
+    import torch
+
+    buf = np.zeros(len(frames) * stride, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        buf[i * stride:i * stride + len(f)] = np.frombuffer(f, dtype=np.uint8)
+    lens = torch.from_numpy(np.array([len(f) for f in frames], dtype=np.uint16).view(np.int16)).to("cuda")
+    return torch.from_numpy(buf).to("cuda"), lens
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1024, 2048, 9216])
+def test_rx_verify_ring_equals_host_path(oracle, stride):
+    """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
+    rest of each slot never read) gives pipck_rx_verify's bits: oracle-checksummed
+    IPv4/IPv6 TCP/UDP/ICMP frames with damage and link padding, edge frames
+    (empty, short, malformed, extension headers past the register window), every
+    frame that fits the slot."""
+    from pip_amd import engine
+
+    rng = random.Random(stride)
+    frames = []
+    for k in range(3000):
+        fam = rng.choice([4, 6])
+        proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
+        l4len = rng.randint(20, min(9000, stride - 80))
+        p = bytearray(_rx_packet(oracle, rng, fam, proto, l4len, k + 1))
+        if k % 3 == 1:
+            p[rng.randrange(len(p))] ^= 0x04
+        frames.append(bytes(p) + rng.randbytes(rng.choice([0, 0, 7])))
+    frames += [b"", bytes(10), bytes([0x45]) + bytes(30), _rx_packet(oracle, rng, 4, 1, 8, 9),
+               _rx_packet(oracle, rng, 6, 17, 300, 2, ext=_ext([(0, 20), (60, 3)], 17))]
+    frames = [f for f in frames if len(f) <= stride]
+    lib, q = _rxq()
+    try:
+        bufs = [C.create_string_buffer(f, max(len(f), 1)) for f in frames]
+        host = _run(lib, q, [C.cast(b, C.c_void_p).value for b in bufs], [len(f) for f in frames])
+    finally:
+        lib.pipck_rxq_destroy(q)
+    ring, lens = _ring(frames, stride)
+    dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+    bad = np.nonzero(dev != host)[0]
+    assert bad.size == 0, [(int(i), frames[i][:48].hex(), int(host[i]), int(dev[i])) for i in bad[:3]]
+    assert (host == VERIFIED).sum() > 1000
+
+
+@pytest.mark.gpu
+def test_rx_verify_ring_full_size():
+    """2M Zipf frames (engine.gen_rx_frames, checksummed by the ragged kernel) in
+    9,216-byte slots: every frame verifies but the zero-checksum UDP ones, and the
+    ring's verdicts equal the byte-packed path's on the same frames."""
+    import torch
+
+    from pip_amd import engine
+
+    n, stride = 2 << 20, 9216
+    ring, lens, kind = engine.gen_rx_ring(n, 31, stride)
+    ok = engine.rx_verify_ring(ring, stride, lens)
+    arena, lens2, tile_off, _, _, _ = engine.gen_rx_frames(n, 31)
+    ok2 = engine.rx_verify_device(arena, lens2, tile_off)
+    assert torch.equal(ok, ok2)
+    n_ok = int((ok == VERIFIED).sum().item())
+    assert n_ok > n - 100 and int((ok == UNCHECKED).sum().item()) == n - n_ok

@@ -65,6 +65,32 @@ def main():
                 fn()
             res[name].append(timed_b2b(fn, a.iters))
             kern[name] = last_kernel().split("(")[0]
+    # rings: frames in fixed-size slots (pipck_rx_verify_ring), sparse (the same
+    # Zipf frames in 9,216-B slots) and dense (1,480-B L4 in 1,536-B slots)
+    for tag, stride, l4_len, m in (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n)):
+        del arena
+        torch.cuda.empty_cache()
+        ring, rlens, _ = engine.gen_rx_ring(m, 11, stride, l4_len=l4_len)
+        rok = torch.empty(m, dtype=torch.uint8, device="cuda")
+        fbytes = int((rlens.to(torch.int64) & 0xFFFF).sum().item())
+
+        def rfn():
+            engine.call("pipck_rx_verify_ring", engine._ptr(ring), stride, engine._ptr(rlens), m, engine._ptr(rok),
+                        engine.current_stream())
+
+        ts = []
+        for _ in range(a.rounds):
+            for _ in range(a.warm):
+                rfn()
+            ts.append(timed_b2b(rfn, a.iters))
+        mr = statistics.median(ts)
+        h = {int(k): int(c) for k, c in zip(*__import__("numpy").unique(rok.cpu().numpy(), return_counts=True))}
+        print(json.dumps({"what": tag, "packets": m, "frame_bytes": fbytes, "slot_bytes": m * stride,
+                          "last_kernel": last_kernel().split("(")[0], "ms": round(mr, 4),
+                          "rounds_ms": [round(x, 4) for x in ts], "GBps": round((fbytes + m) / mr / 1e6, 1),
+                          "frac": round((fbytes + m) / mr / 1e6 / 8000, 4), "verdicts": h}), flush=True)
+        del ring
+        arena = torch.empty(1, device="cuda")
     v = ok.cpu().numpy()
     hist = {int(k): int(c) for k, c in zip(*__import__("numpy").unique(v, return_counts=True))}
     for name, ms in res.items():
