@@ -96,6 +96,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         const uint32_t L = pk < np ? s_len[pk] : 0u;
         // past the frame: an offset beyond the resource, which reads zeros with
         // no memory request (a predicated load would make every row wait vmcnt(0))
+        // (skipping the load of a row past every frame, a wave-uniform branch,
+        // turned every wait of the ring into vmcnt(0): the load always issues)
         return buf_load<true>(tb, 16u * k < L ? ((w + 4u * j) * 64u + (uint32_t)lane) * 16u : 0xFFFFFFF0u);
     };
     u32x4 v[kRingU];
@@ -115,11 +117,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     pk++;
                 }
                 const uint32_t L = pk < np ? s_len[pk] : 0u;
-                u32x4 x = v[u];
-                if (16u * k + 16u > L) x = 16u * k < L ? mask_tail(x, (int)(L - 16u * k)) : u32x4{0u, 0u, 0u, 0u};
-                if (pk < np) {
+                // only chunks inside a frame add anything: a row past every
+                // lane's frame (most rows of a sparse ring) does no LDS work
+                if (16u * k < L) {
+                    u32x4 x = v[u];
+                    if (16u * k + 16u > L) x = mask_tail(x, (int)(L - 16u * k));
                     atomicAdd(&part[pk], dot4(x, 0u));
-                    if (k < 6u) hdr[k * K + pk] = x;  // the slot's header window (bytes past the frame zero)
+                    if (k < 6u) hdr[k * K + pk] = x;  // the slot's header window
                 }
                 step(pkt, k0);
             }
