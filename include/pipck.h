@@ -278,12 +278,12 @@ int pipck_host_checksum_packed_bytes(pipck_ctx* ctx, const void* h_arena, const 
 /* This context's per-packet path (pipck_host_sum): 0 = staged (H2D copy,
  * kernel, D2H copy), 1 = zero-copy (the kernel reads the pinned, coherent
  * staging buffer and writes the result to pinned host memory), 2 = auto
- * (zero-copy up to 64 KiB of staged bytes; the mode of a new context),
- * 3 = resident (up to 64 KiB: one 256-thread block of this context stays on
+ * (zero-copy up to 68 KiB of staged bytes -- any single IP datagram; the
+ * mode of a new context), 3 = resident (up to 68 KiB: one 256-thread block of this context stays on
  * the GPU, polls a doorbell in pinned host memory and answers without a
  * launch; it exits after 10 ms without a call, or when the mode changes or
  * the context is destroyed, and relaunches on the next call; larger calls take
- * the zero-copy launch), 4 = resident with the doorbell in fine-grained device
+ * the staged copies), 4 = resident with the doorbell in fine-grained device
  * memory the host writes directly (large-BAR systems; falls back to mode 3's
  * pinned doorbell where that allocation fails).  Every path computes the same
  * result.  Nothing is read from the environment.

@@ -100,8 +100,8 @@ def test_every_known_answer_on_gpu_zero_copy(kat):
 def test_every_known_answer_on_gpu_resident(kat, mode):
     """The same known answers through the resident service (mode 3: one block
     stays on the GPU polling a doorbell in pinned host memory; mode 4: the
-    doorbell in fine-grained device memory; requests over 64 KiB -- the
-    131,076-B wrap KATs -- take the zero-copy launch).  The block's idle exit
+    doorbell in fine-grained device memory; requests over 68 KiB -- the
+    131,076-B wrap KATs -- take the staged copies).  The block's idle exit
     and relaunch are exercised too: a pause longer than its 10 ms idle timeout,
     then more calls; then mode changes (each ends the block)."""
     import time
