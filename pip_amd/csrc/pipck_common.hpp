@@ -99,6 +99,8 @@ int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t*
 // The one-packet-per-wave measurement arm (pipck_wave.hip; pipck_tune
 // lanes_per_packet == kWaveArm): fixed strides (desc == false) or descriptors.
 constexpr uint32_t kWaveArm = 256;
+bool wave_arm();  // pipck_tune(kWaveArm, ...) is in force (pipck_kernels.hip)
+bool alt_schedule();  // pipck_tune flag bit 28 (the other schedule) is set
 int launch_wave(bool verify, bool desc, const void* d_arena, uint64_t stride, uint32_t len, const pipck_desc* d_desc,
                 uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                 uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s,

@@ -1426,6 +1426,8 @@ struct Tune {
     std::atomic<uint32_t> lanes{0}, loads{0}, blocks{0}, flags{0};
 };
 static Tune g_tune;
+bool wave_arm() { return g_tune.lanes.load() == kWaveArm; }
+bool alt_schedule() { return (g_tune.flags.load() >> 28) & 1u; }
 
 // The batch kernel this thread launched last (pipck_common.hpp, PIPCK_LAUNCH).
 thread_local const void* t_last_kernel = nullptr;

@@ -150,6 +150,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     }
 }
 
+// ---- the same ring, slot by slot (sparse rings: short frames in large slots) --
+// k_ring_rx walks every row of every slot: a row past every lane's frame still
+// issues its (range-checked, request-free) load and index math, so a ring of
+// ~1 KB frames in 9,216-B slots costs the slot rows, not the frame bytes.
+// k_ring_slots gives each wave kSlotG slots and touches only each frame's
+// chunks: the first row (64 chunks = 1 KiB) of all kSlotG frames is in flight
+// at once, a frame longer than 1 KiB then streams its further rows 4 at a time,
+// and one wave reduce per slot gives its sum.  Lanes 0-5 of the first row are
+// the header window; the block's 32 slots are judged by its first 32 threads.
+// The default for slots of 4 KiB and more (launch_ring_rx).
+constexpr int kSlotG = 8;
+
+__global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ arena, uint32_t cpp,
+                                                    const uint16_t* __restrict__ lens, uint64_t n,
+                                                    uint8_t* __restrict__ ok) {
+    __shared__ u32x4 s_hdr[6][4 * kSlotG];
+    __shared__ uint32_t s_sum[4 * kSlotG], s_len[4 * kSlotG];
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t b0 = (uint64_t)blockIdx.x * (4u * kSlotG);
+    const uint64_t p0 = b0 + w * kSlotG;  // this wave's first slot
+    const uint32_t lmine = (lane < kSlotG && p0 + (uint32_t)lane < n) ? (uint32_t)lens[p0 + lane] : 0u;
+    uint32_t L[kSlotG], Lc[kSlotG];
+    buf_t r[kSlotG];
+    u32x4 v[kSlotG];
+#pragma unroll
+    for (int g = 0; g < kSlotG; g++) {
+        L[g] = (uint32_t)__builtin_amdgcn_readlane((int)lmine, g);
+        Lc[g] = min(L[g], 16u * cpp);  // the slot bounds the bytes read
+        r[g] = buf_rsrc(arena + (p0 + g) * cpp * 16u, (Lc[g] + 15u) & ~15u);  // slots past n: L = 0
+        v[g] = buf_load<true>(r[g], (uint32_t)lane * 16u);
+    }
+#pragma unroll
+    for (int g = 0; g < kSlotG; g++) {
+        const int hi = (int)Lc[g] - 16 * lane;
+        const u32x4 x = hi < 16 ? mask_tail(v[g], hi) : v[g];  // past the frame: zeros
+        uint32_t acc = dot4(x, 0u);
+        if (lane < 6) s_hdr[lane][w * kSlotG + g] = x;
+        const uint32_t nch = (Lc[g] + 15u) >> 4;
+        for (uint32_t c0 = 64; c0 < nch; c0 += 256) {  // wave-uniform: frames over 1 KiB
+            u32x4 e[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[k] = buf_load<true>(r[g], (c0 + 64u * k + (uint32_t)lane) * 16u);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int h = (int)Lc[g] - 16 * (int)(c0 + 64u * k + (uint32_t)lane);
+                acc = dot4(h < 16 ? mask_tail(e[k], h) : e[k], acc);
+            }
+        }
+        const uint32_t s = wave_total(acc);
+        if (lane == 0) {
+            s_sum[w * kSlotG + g] = s;
+            s_len[w * kSlotG + g] = L[g];
+        }
+    }
+    __syncthreads();
+    const uint32_t i = threadIdx.x;
+    const uint32_t np = (uint32_t)min<uint64_t>(4u * kSlotG, n - b0);
+    if (i < np) {
+        const uint32_t Li = s_len[i];
+        const uint32_t F = bswap16(fold16(s_sum[i]));  // slots start 16-byte aligned: even address
+        uint32_t hw[24];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const u32x4 x = s_hdr[k][i];
+            hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
+        }
+        const uint8_t* pkp = arena + (b0 + i) * cpp * 16u;
+        store_result8(buf_rsrc(ok + b0, np), i, rx_from_window(pkp, Li, F, hw));
+    }
+}
+
 int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
                    hipStream_t s) {
     if (n == 0) return PIPCK_OK;
@@ -163,6 +235,21 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         return PIPCK_EINVAL;
     }
     const uint32_t cpp = (uint32_t)(stride / 16);
+    // slot by slot from 4 KiB slots (a sparse 9,216-B ring of cfg4's Zipf frames
+    // 7.01 -> 1.34 ms, a full one even; full 1,536-B slots 0.81 by rows against
+    // 0.72, profiles/r04_ring_schedule_ab.jsonl); pipck_tune's wave-per-packet arm
+    // forces it, flag bit 28 (the other schedule) the row stream
+    if (wave_arm() || (stride >= 4096 && !alt_schedule())) {
+        const uint64_t blocks = (n + 4u * kSlotG - 1) / (4u * kSlotG);
+        if (blocks > 0x7FFFFFFFull) {
+            set_error("pipck_rx_verify_ring: too many slots for one launch");
+            return PIPCK_ERANGE;
+        }
+        PIPCK_LAUNCH(k_ring_slots, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)d_arena, cpp, d_lens, n,
+                     d_ok);
+        PIPCK_LAUNCHED("k_ring_slots");
+        return PIPCK_OK;
+    }
     // K slots per block task: ~4 waves x 48 rows (x 64 for jumbo slots), a
     // multiple of 8, at most 256 (one slot per thread at the end) -- k_flat_coop's
     uint32_t K = (4u * (cpp >= 256 ? 64u : 48u) * 64u) / cpp;

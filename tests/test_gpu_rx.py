@@ -415,8 +415,9 @@ def _ring(frames, stride):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slots", [False, True], ids=["rows", "slots"])
 @pytest.mark.parametrize("stride", [1024, 2048, 9216])
-def test_rx_verify_ring_equals_host_path(oracle, stride):
+def test_rx_verify_ring_equals_host_path(oracle, stride, slots):
     """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
     rest of each slot never read) gives pipck_rx_verify's bits: oracle-checksummed
     IPv4/IPv6 TCP/UDP/ICMP frames with damage and link padding, edge frames
@@ -444,14 +445,30 @@ def test_rx_verify_ring_equals_host_path(oracle, stride):
     finally:
         lib.pipck_rxq_destroy(q)
     ring, lens = _ring(frames, stride)
-    dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+    # both schedules: the row stream (k_ring_rx) and slot by slot (k_ring_slots,
+    # the wave-per-packet arm)
+    engine.tune(lanes_per_packet=256) if slots else engine.tune(alt_flat_schedule=True)
+    try:
+        dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+        assert ("k_ring_slots" if slots else "k_ring_rx") in _last_kernel()
+    finally:
+        engine.tune()
     bad = np.nonzero(dev != host)[0]
     assert bad.size == 0, [(int(i), frames[i][:48].hex(), int(host[i]), int(dev[i])) for i in bad[:3]]
     assert (host == VERIFIED).sum() > 1000
 
 
+def _last_kernel():
+    buf = C.create_string_buffer(4096)
+    from pip_amd import _lib
+
+    _lib.check("pipck_last_launch", _lib.load().pipck_last_launch(buf, len(buf)))
+    return buf.value.decode()
+
+
 @pytest.mark.gpu
-def test_rx_verify_ring_full_size():
+@pytest.mark.parametrize("slots", [False, True], ids=["rows", "slots"])
+def test_rx_verify_ring_full_size(slots):
     """2M Zipf frames (engine.gen_rx_frames, checksummed by the ragged kernel) in
     9,216-byte slots: every frame verifies but the zero-checksum UDP ones, and the
     ring's verdicts equal the byte-packed path's on the same frames."""
@@ -461,9 +478,44 @@ def test_rx_verify_ring_full_size():
 
     n, stride = 2 << 20, 9216
     ring, lens, kind = engine.gen_rx_ring(n, 31, stride)
-    ok = engine.rx_verify_ring(ring, stride, lens)
+    engine.tune(lanes_per_packet=256) if slots else engine.tune(alt_flat_schedule=True)
+    try:
+        ok = engine.rx_verify_ring(ring, stride, lens)
+    finally:
+        engine.tune()
     arena, lens2, tile_off, _, _, _ = engine.gen_rx_frames(n, 31)
     ok2 = engine.rx_verify_device(arena, lens2, tile_off)
     assert torch.equal(ok, ok2)
     n_ok = int((ok == VERIFIED).sum().item())
     assert n_ok > n - 100 and int((ok == UNCHECKED).sum().item()) == n - n_ok
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride,kernel", [(1024, "k_ring_rx"), (2048, "k_ring_rx"), (4080, "k_ring_rx"),
+                                           (4096, "k_ring_slots"), (9216, "k_ring_slots")])
+def test_rx_verify_ring_default_schedule(oracle, stride, kernel):
+    """The ring's default schedule by slot size (the row stream below 4 KiB, slot by
+    slot from 4 KiB), and its verdicts equal the other schedule's on the same
+    ring: 1,000 oracle-checksummed frames, a third damaged, n not a multiple of
+    the 32 slots of a k_ring_slots block."""
+    from pip_amd import engine
+
+    rng = random.Random(stride + 7)
+    frames = []
+    for k in range(1001):
+        fam = rng.choice([4, 6])
+        p = bytearray(_rx_packet(oracle, rng, fam, rng.choice([6, 17]), rng.randint(20, stride - 80), k + 1))
+        if k % 3 == 1:
+            p[rng.randrange(len(p))] ^= 0x10
+        frames.append(bytes(p))
+    ring, lens = _ring(frames, stride)
+    dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+    assert kernel in _last_kernel()
+    engine.tune(lanes_per_packet=256) if kernel == "k_ring_rx" else engine.tune(alt_flat_schedule=True)
+    try:
+        other = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+        assert kernel not in _last_kernel()
+    finally:
+        engine.tune()
+    assert np.array_equal(dev, other)
+    assert 600 < int((dev == VERIFIED).sum()) < 700

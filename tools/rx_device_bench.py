@@ -67,7 +67,7 @@ def main():
             kern[name] = last_kernel().split("(")[0]
     # rings: frames in fixed-size slots (pipck_rx_verify_ring), sparse (the same
     # Zipf frames in 9,216-B slots) and dense (1,480-B L4 in 1,536-B slots)
-    for tag, stride, l4_len, m in (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n)):
+    for tag, stride, l4_len, m in (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n), ("ring_dense_9216", 9216, 8900, n // 2)):
         del arena
         torch.cuda.empty_cache()
         ring, rlens, _ = engine.gen_rx_ring(m, 11, stride, l4_len=l4_len)
@@ -78,17 +78,28 @@ def main():
             engine.call("pipck_rx_verify_ring", engine._ptr(ring), stride, engine._ptr(rlens), m, engine._ptr(rok),
                         engine.current_stream())
 
-        ts = []
+        # both schedules, forced: the row stream (k_ring_rx, flag bit 28) and slot by
+        # slot (k_ring_slots, the wave-per-packet arm), rounds interleaved, verdicts
+        # equal (the default: slots from 4 KiB)
+        ts = {"rows": [], "slots": []}
+        got = {}
         for _ in range(a.rounds):
-            for _ in range(a.warm):
-                rfn()
-            ts.append(timed_b2b(rfn, a.iters))
-        mr = statistics.median(ts)
-        h = {int(k): int(c) for k, c in zip(*__import__("numpy").unique(rok.cpu().numpy(), return_counts=True))}
-        print(json.dumps({"what": tag, "packets": m, "frame_bytes": fbytes, "slot_bytes": m * stride,
-                          "last_kernel": last_kernel().split("(")[0], "ms": round(mr, 4),
-                          "rounds_ms": [round(x, 4) for x in ts], "GBps": round((fbytes + m) / mr / 1e6, 1),
-                          "frac": round((fbytes + m) / mr / 1e6 / 8000, 4), "verdicts": h}), flush=True)
+            for arm in ts:
+                engine.tune(lanes_per_packet=256) if arm == "slots" else engine.tune(alt_flat_schedule=True)
+                for _ in range(a.warm):
+                    rfn()
+                ts[arm].append(timed_b2b(rfn, a.iters))
+                got[arm] = (last_kernel().split("(")[0], rok.clone())
+        engine.tune()
+        assert torch.equal(got["rows"][1], got["slots"][1])
+        for arm, tl in ts.items():
+            mr = statistics.median(tl)
+            h = {int(k): int(c) for k, c in zip(*__import__("numpy").unique(got[arm][1].cpu().numpy(), return_counts=True))}
+            print(json.dumps({"what": tag, "schedule": arm, "packets": m, "frame_bytes": fbytes,
+                              "slot_bytes": m * stride, "last_kernel": got[arm][0], "ms": round(mr, 4),
+                              "rounds_ms": [round(x, 4) for x in tl], "GBps": round((fbytes + m) / mr / 1e6, 1),
+                              "frac": round((fbytes + m) / mr / 1e6 / 8000, 4), "verdicts": h,
+                              "verdicts_equal_across_schedules": True}), flush=True)
         del ring
         arena = torch.empty(1, device="cuda")
     v = ok.cpu().numpy()
