@@ -40,7 +40,8 @@ namespace pipck {
 
 // ---- frames in fixed-size slots (a receive ring: slot i at arena + i * stride,
 // lens[i] bytes of frame in it, the rest of the slot unused) -----------------
-// k_ring_rx streams the slots like k_flat_coop (pipck_coop.hip): a block task
+// k_ring_rx (the row stream; launch_ring_rx's default is k_ring_slots below)
+// streams the slots like k_flat_coop (pipck_coop.hip): a block task
 // of K whole slots, its four waves on interleaved 1 KiB rows, a ring of U rows
 // per wave, one LDS partial per lane per slot.  Unlike k_flat_coop each lane's
 // load is predicated on the chunk lying inside its slot's frame (the slot's
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // at once, a frame longer than 1 KiB then streams its further rows 4 at a time,
 // and one wave reduce per slot gives its sum.  Lanes 0-5 of the first row are
 // the header window; the block's 32 slots are judged by its first 32 threads.
-// The default for slots of 4 KiB and more (launch_ring_rx).
+// The default schedule (launch_ring_rx).
 constexpr int kSlotG = 8;
 
 __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ arena, uint32_t cpp,
@@ -235,11 +236,14 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         return PIPCK_EINVAL;
     }
     const uint32_t cpp = (uint32_t)(stride / 16);
-    // slot by slot from 4 KiB slots (a sparse 9,216-B ring of cfg4's Zipf frames
-    // 7.01 -> 1.34 ms, a full one even; full 1,536-B slots 0.81 by rows against
-    // 0.72, profiles/r04_ring_schedule_ab.jsonl); pipck_tune's wave-per-packet arm
-    // forces it, flag bit 28 (the other schedule) the row stream
-    if (wave_arm() || (stride >= 4096 && !alt_schedule())) {
+    // slot by slot (k_ring_slots) by default: a sparse 9,216-B ring of cfg4's
+    // Zipf frames 7.01 -> 1.33 ms, ~260-B frames in 2 KiB slots 1.90 -> 0.62,
+    // ~160-B frames in 1 KiB slots 1.80 -> 0.62; the row stream wins only on
+    // full slots (1,536-B: 0.83 against 0.73; 9,216-B: 0.87 against 0.85),
+    // profiles/r04_ring_schedule_ab.jsonl.  A ring's fill is not known at launch,
+    // and a 13 % loss on full rings weighs less than a 3-5x loss on sparse ones.
+    // pipck_tune flag bit 28 (the other schedule) selects the row stream.
+    if (wave_arm() || !alt_schedule()) {
         const uint64_t blocks = (n + 4u * kSlotG - 1) / (4u * kSlotG);
         if (blocks > 0x7FFFFFFFull) {
             set_error("pipck_rx_verify_ring: too many slots for one launch");

@@ -49,9 +49,8 @@ extern "C" {
  * Bits 21-23 launch separate probe kernels (k_flat_probe, k_flat_coop_probe:
  * checksum mode, non-temporal loads, rings 24/32 for k_flat); the production
  * kernels have them compiled out and ignore them otherwise.
- * Bit 28 = the other fixed-stride schedule (and for pipck_rx_verify_ring at
- * slots of 4 KiB or more the row stream k_ring_rx, whose default there is
- * k_ring_slots; lanes_per_packet 256 forces k_ring_slots): k_flat (one task per wave)
+ * Bit 28 = the other fixed-stride schedule (and for pipck_rx_verify_ring the
+ * row stream k_ring_rx instead of the default k_ring_slots): k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
  * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
  * for k_flat_coop, bits 8..15 are rows per wave

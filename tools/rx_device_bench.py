@@ -66,8 +66,11 @@ def main():
             res[name].append(timed_b2b(fn, a.iters))
             kern[name] = last_kernel().split("(")[0]
     # rings: frames in fixed-size slots (pipck_rx_verify_ring), sparse (the same
-    # Zipf frames in 9,216-B slots) and dense (1,480-B L4 in 1,536-B slots)
-    for tag, stride, l4_len, m in (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n), ("ring_dense_9216", 9216, 8900, n // 2)):
+    # Zipf frames in 9,216-B slots), dense (1,480-B L4 in 1,536-B slots, 8,900-B
+    # L4 in 9,216-B slots) and short frames in small slots (200-B L4 in 2 KiB,
+    # 100-B L4 in 1 KiB)
+    for tag, stride, l4_len, m in (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n), ("ring_dense_9216", 9216, 8900, n // 2),
+                                   ("ring_short_2048", 2048, 200, n), ("ring_short_1024", 1024, 100, n)):
         del arena
         torch.cuda.empty_cache()
         ring, rlens, _ = engine.gen_rx_ring(m, 11, stride, l4_len=l4_len)
