@@ -48,7 +48,13 @@ extern "C" {
 
 /* Human-readable text of the last error on the calling thread. */
 const char* pipck_last_error(void);
-/* ABI version, (major << 16) | minor. */
+/* ABI version, (major << 16) | minor (PIPCK_VERSION_MAJOR / _MINOR of this
+ * header; a minor step only adds entry points).  1.1: the RX verdicts are the
+ * 3-bit PIPCK_RX_* values (7 = verified; 3 = nothing failed, payload NOT
+ * checked) -- 1.0's single "ok == 3" meant verified.  1.2: the bounded _n forms
+ * of the ragged, chain and ring calls. */
+#define PIPCK_VERSION_MAJOR 1
+#define PIPCK_VERSION_MINOR 2
 uint32_t pipck_version(void);
 
 /* ---- flows / pseudo-headers ------------------------------------------ */
@@ -99,9 +105,20 @@ typedef struct pipck_desc {
 } pipck_desc;
 
 /* d_err (optional, device u32): OR-ed with (1 << PIPCK_ERANGE) when a
- * descriptor is out of domain; that packet's result is then 0. */
+ * descriptor is out of domain; that packet's result is then 0.  This form
+ * trusts the descriptors' offsets and flows (only len > 65535 is refused). */
 int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
                           const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_err, void* stream);
+/* Bounded form: arena_bytes = the arena's size (readable from the 16-byte
+ * boundary at or below d_arena to the one at or above d_arena + arena_bytes);
+ * with d_pseudo, n_flows = its entries (> 0).  A descriptor whose bytes
+ * [offset, offset + len) pass arena_bytes (overflow-safe), whose len exceeds
+ * 65535 or whose flow is >= n_flows -- a stale or foreign descriptor -- is not
+ * read: its result is 0 and d_err gets (1 << PIPCK_ERANGE).  The plain name
+ * above is this with arena_bytes and n_flows unbounded. */
+int pipck_checksum_ragged_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_desc, uint64_t n_packets,
+                            const uint32_t* d_pseudo, uint32_t n_flows, uint16_t* d_out, uint32_t* d_err,
+                            void* stream);
 
 /* Packed ragged batch: per-packet lengths, no per-packet descriptors.
  * Packets lie back to back, each starting 16-byte aligned where the previous
@@ -182,6 +199,16 @@ int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_
                           const uint64_t* d_seg_begin, const uint32_t* d_pkt_flow, uint64_t n_packets,
                           const uint32_t* d_pseudo, uint32_t* d_scratch, uint16_t* d_out, uint32_t* d_err,
                           void* stream);
+/* Bounded form, as pipck_checksum_ragged_n for every segment (arena_bytes) and
+ * every d_pkt_flow entry (n_flows, > 0 with d_pseudo): a packet holding a
+ * refused segment, or with a flow past the table, gets 0 and d_err gets
+ * (1 << PIPCK_ERANGE).  In both forms a packet whose [d_seg_begin[p],
+ * d_seg_begin[p+1]) is not inside [0, n_segs] gets 0 and sets the same bit --
+ * no segment record outside the scratch is read. */
+int pipck_checksum_chains_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_segs, uint64_t n_segs,
+                            const uint64_t* d_seg_begin, const uint32_t* d_pkt_flow, uint64_t n_packets,
+                            const uint32_t* d_pseudo, uint32_t n_flows, uint32_t* d_scratch, uint16_t* d_out,
+                            uint32_t* d_err, void* stream);
 
 /* RX verification (a capability pip lacks): same
  * inputs as pipck_checksum_fixed but the packets carry their checksum field;
@@ -194,6 +221,9 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
  * out-of-domain descriptors verify as 0 and set d_err. */
 int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
                         const uint32_t* d_pseudo, uint8_t* d_ok, uint32_t* d_err, void* stream);
+/* Bounded form, as pipck_checksum_ragged_n. */
+int pipck_verify_ragged_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_desc, uint64_t n_packets,
+                          const uint32_t* d_pseudo, uint32_t n_flows, uint8_t* d_ok, uint32_t* d_err, void* stream);
 
 /* Incremental update for header rewrites (RFC 1624, SURVEY.md section 8 f4;
  * replaces a full re-run of pip_standard_checksum, pip_checksum.cpp:13-33,
@@ -408,16 +438,28 @@ int pipck_rx_verify(pipck_rxq* q, const void* const* pkts, const uint32_t* lens,
  * boundary after the last frame.  Bounded as pipck_checksum_packed_bytes_n: a tile
  * reaching past arena_bytes is not read, its packets get 0 and d_err
  * (optional) gets (1 << PIPCK_ERANGE).  Asynchronous. */
-/* The same for frames in the fixed-size slots of a receive ring in DEVICE
- * memory: frame i (d_lens[i] <= slot_stride bytes) at d_arena + i *
- * slot_stride, the rest of each slot unused and never read.  d_arena 16-byte
- * aligned; slot_stride a multiple of 16 from 1,024 to 65,536 (PIPCK_EINVAL
- * otherwise).  One kernel on `stream`; d_ok[i] as pipck_rx_verify_device. */
+int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
+                           const uint64_t* d_tile_off, uint64_t n_packets, uint8_t* d_ok, uint32_t* d_err,
+                           void* stream);
+
+/* The same verdicts for frames in the fixed-size slots of a receive ring in
+ * DEVICE memory: frame i of d_lens[i] bytes at d_arena + i * slot_stride, the
+ * rest of each slot unused and never read.  d_arena 16-byte aligned, readable
+ * for n_slots * slot_stride bytes; slot_stride a multiple of 16 from 1,024 to
+ * 65,536 (PIPCK_EINVAL otherwise).  The lengths are bounded on the device: a
+ * slot with d_lens[i] > slot_stride (a corrupt or foreign length) is not read
+ * at all -- no load and no header parse leaves its slot -- gets d_ok[i] = 0,
+ * and d_err (optional, device u32) gets (1 << PIPCK_ERANGE).  One kernel on
+ * `stream`, asynchronous; d_ok[i] as pipck_rx_verify_device. */
+int pipck_rx_verify_ring_n(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n_slots,
+                           uint8_t* d_ok, uint32_t* d_err, void* stream);
+/* pipck_rx_verify_ring_n without the error word (slots are bounded the same way). */
 int pipck_rx_verify_ring(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n_slots,
                          uint8_t* d_ok, void* stream);
-/* The same for received frames back to back in HOST memory (a receive buffer
- * read in order, a capture file's records): chunks of ~64 MiB go H2D by DMA
- * with their u16 lengths, pipck_rx_verify_device judges them, the verdicts
+
+/* The same verdicts for received frames back to back in HOST memory (a receive
+ * buffer read in order, a capture file's records): chunks of ~64 MiB go H2D by
+ * DMA with their u16 lengths, pipck_rx_verify_device judges them, the verdicts
  * come back; double-buffered over the context's two streams, PCIe-bound at
  * every frame size (pipck_rx_verify reads each packet in place with a wave of
  * its own: better for scattered packets, slower for small ones).  h_frames
@@ -425,9 +467,6 @@ int pipck_rx_verify_ring(const void* d_arena, uint64_t slot_stride, const uint16
  * *n_verified (optional) = frames with ok == PIPCK_RX_VERIFIED. */
 int pipck_host_rx_verify_packed(pipck_ctx* ctx, const void* h_frames, const uint16_t* h_lens, uint64_t n_frames,
                                 uint8_t* h_ok, uint64_t* n_verified);
-int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
-                           const uint64_t* d_tile_off, uint64_t n_packets, uint8_t* d_ok, uint32_t* d_err,
-                           void* stream);
 
 #ifdef __cplusplus
 }

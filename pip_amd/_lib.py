@@ -103,11 +103,16 @@ SIGNATURES = {
     "pipck_rx_verify_device": (_i32, [_p, _u64, _p, _p, _u64, _p, _p, _p]),
     "pipck_host_rx_verify_packed": (_i32, [_p, _p, _p, _u64, _p, C.POINTER(_u64)]),
     "pipck_rx_verify_ring": (_i32, [_p, _u64, _p, _u64, _p, _p]),
+    "pipck_rx_verify_ring_n": (_i32, [_p, _u64, _p, _u64, _p, _p, _p]),
+    "pipck_checksum_ragged_n": (_i32, [_p, _u64, _p, _u64, _p, _u32, _p, _p, _p]),
+    "pipck_verify_ragged_n": (_i32, [_p, _u64, _p, _u64, _p, _u32, _p, _p, _p]),
+    "pipck_checksum_chains_n": (_i32, [_p, _u64, _p, _u64, _p, _p, _u64, _p, _u32, _p, _p, _p, _p]),
 }
 
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only
 INTERNAL_SIGNATURES = {
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
+    "pipck_tune_probes": (None, [_u32]),
     "pipck_trace_tasks": (_i32, [_p, _u64]),
     "pipck_tune_xcd_weights": (_i32, [_p, _u32]),
     "pipck_last_launch": (_i32, [C.c_char_p, _sz]),

@@ -78,7 +78,8 @@ void pinned_release(PinnedRec& r);
 // the TX queue mixes its device staging copy with zero-copy pinned host segments.
 int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
                      const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo, uint32_t* d_scratch,
-                     uint16_t* d_out, uint32_t* d_err, hipStream_t s);
+                     uint16_t* d_out, uint32_t* d_err, hipStream_t s, uint64_t arena_bytes = UINT64_MAX,
+                     uint32_t n_flows = UINT32_MAX);
 
 // The block-cooperative flat stream (pipck_coop.hip); PIPCK_EINVAL when the
 // shape does not fit its block tasks (the caller then takes k_flat).
@@ -93,6 +94,8 @@ int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, 
                uint8_t* d_ok, hipStream_t s, uint32_t rows, uint32_t ring, bool nt, uint32_t kflags, bool coop = false);
 
 // pipck_rx_verify_device (pipck_packedb.hip): k_packedb with the RX verdicts.
+int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
+                   uint32_t* d_err, hipStream_t s);
 int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens, const uint64_t* d_tile_off,
                       uint64_t n, uint8_t* d_ok, uint32_t* d_err, hipStream_t s);
 
@@ -101,9 +104,14 @@ int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t*
 constexpr uint32_t kWaveArm = 256;
 bool wave_arm();  // pipck_tune(kWaveArm, ...) is in force (pipck_kernels.hip)
 bool alt_schedule();  // pipck_tune flag bit 28 (the other schedule) is set
+uint32_t g_tune_flags();  // pipck_tune's flags / loads_per_lane in force
+uint32_t g_tune_loads();
+// measurement-only probes that change results (pipck_tune_probes, pipck_testing.h)
+constexpr uint32_t kProbeHdrInPlace = 1u;
+extern std::atomic<uint32_t> g_probes;
 int launch_wave(bool verify, bool desc, const void* d_arena, uint64_t stride, uint32_t len, const pipck_desc* d_desc,
                 uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                 uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s,
-                uint32_t max_chunks, uint32_t nl);
+                uint32_t max_chunks, uint32_t nl, uint64_t arena_bytes = UINT64_MAX);
 
 }  // namespace pipck

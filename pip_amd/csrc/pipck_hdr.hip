@@ -38,12 +38,13 @@ namespace pipck {
 constexpr uint32_t kHdrPlainStores = 1u << 29;
 constexpr uint32_t kHdrNtStores = 1u << 30;
 constexpr uint32_t kHdrNarrowStores = 1u << 31;
-// bit 28, measurement only: store each header's checksum
+// measurement only (pipck_tune_probes, not a tune flag --
+// the flags' settings all compute the same results): store each header's checksum
 // INTO the header -- htons(result) at byte 10, its ip_sum, as pip_netif.cpp:97
 // stores it -- instead of into the result array (which is left untouched): the
 // "results inside the headers" layout, to weigh its write-back of whole dirty
 // lines against the separate 2-byte result stream.
-constexpr uint32_t kHdrInPlace = 1u << 28;
+constexpr uint32_t kHdrInPlace = 1u << 28;  // the kernel's own flag word only (launch_hdr sets it)
 
 template <int D>
 struct HdrGeom {
@@ -210,6 +211,9 @@ int launch_hdr(bool verify, const void* d_arena, uint64_t stride, uint32_t len, 
     if (blocks > 0x7FFFFFFFull || per * stride >= (1ull << 31)) return PIPCK_EINVAL;
     const size_t lds = 4u * per * sizeof(uint16_t);
     const uint32_t u = ring ? ring : 32u;
+    // bit 28 of the tune flags is the other fixed-stride schedule elsewhere (same
+    // results); here it carries the in-place probe only when that probe is on
+    kflags = (kflags & ~kHdrInPlace) | ((g_probes.load() & kProbeHdrInPlace) ? kHdrInPlace : 0u);
     const int ui = u >= 32 ? 3 : (u >= 24 ? 2 : (u >= 16 ? 1 : 0));
 #define PIPCK_HD(D, U, CO) {{k_hdr<D, U, false, false, CO>, k_hdr<D, U, false, true, CO>}, \
                            {k_hdr<D, U, true, false, CO>, k_hdr<D, U, true, true, CO>}}

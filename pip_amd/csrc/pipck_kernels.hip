@@ -936,6 +936,9 @@ struct RaggedTileLds {
 };
 
 constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
+// k_ragged's per-segment record (len << 16 | F) of a refused chain segment:
+// length 0 with a nonzero sum, which no real segment has
+constexpr uint32_t kBadSeg = 0x0000FFFFu;
 // A tile whose segments all span <= 2 chunks (20-B IPv4 headers) is summed
 // lane-per-segment: 1.36 -> 1.69 TB/s on 20-B segments; at 3 chunks (40 B)
 // the chunk stream is 3 % faster (profiles/r01_ragged_shapes6_tiny.jsonl).
@@ -1245,7 +1248,7 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
                                                 uint64_t n, const uint32_t* __restrict__ pseudo,
                                                 uint16_t* __restrict__ out, uint32_t* __restrict__ fseg,
                                                 uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
-                                                uint32_t kflags) {
+                                                uint32_t kflags, uint64_t arena_bytes, uint32_t n_flows) {
     __shared__ RaggedTileLds s_tile[WPB];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     RaggedTileLds& t = s_tile[w];
@@ -1260,10 +1263,13 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
         // prefetch the next tile's descriptors; they land while this tile streams
         const uint64_t nseg = (tile + tr.step) * 64 + lane;
         if (tile + tr.step < tr.end) dn = nseg < n ? desc[nseg] : pipck_desc{0, 0, 0};
-        const bool bad = valid && d.len > PIPCK_MAX_SEG_LEN;
+        // out of domain: longer than 65535 B, bytes past the arena (overflow-safe),
+        // or a flow past the table -- not read, result 0, PIPCK_ERANGE in err
+        const bool bad = valid && (d.len > PIPCK_MAX_SEG_LEN || d.offset > arena_bytes ||
+                                   (uint64_t)d.len > arena_bytes - d.offset || (FINAL && pseudo && d.flow >= n_flows));
         const uint32_t len = (valid && !bad) ? d.len : 0u;
         // the flow's pseudo-header base, loaded now so the tile's end waits on nothing
-        const uint32_t Pbase = FINAL && pseudo && valid ? pseudo[d.flow] : 0u;
+        const uint32_t Pbase = FINAL && pseudo && valid && !bad ? pseudo[d.flow] : 0u;
         const uintptr_t addr = (uintptr_t)arena + d.offset;
         const uint32_t head = (uint32_t)(addr & 15);
         const uint32_t nch = len ? (head + len + 15) >> 4 : 0u;
@@ -1283,7 +1289,9 @@ __global__ __launch_bounds__(256) void k_ragged(const uint8_t* __restrict__ aren
                 else
                     out[seg] = bad ? (uint16_t)0 : finish(P, F);
             } else {
-                fseg[seg] = (len << 16) | F;  // len <= 65535 (bad segments: len 0, flagged in err)
+                // len <= 65535; a bad segment gets kBadSeg (length 0 with a nonzero
+                // sum: no real segment) so k_chain_finish zeroes its packet
+                fseg[seg] = bad ? kBadSeg : (len << 16) | F;
             }
             if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
         }
@@ -1404,18 +1412,31 @@ __global__ __launch_bounds__(1024) void k_packed_tile_scan(uint64_t* __restrict_
 
 // Per packet: the segments' folded sums and lengths, packed by k_ragged as
 // (len << 16) | F, so no descriptor is read again.
+// A packet whose segment range is not inside [0, n_segs], whose flow is past
+// the table, or holding a segment k_ragged refused (kBadSeg) gets 0 and sets
+// PIPCK_ERANGE in err.
 __global__ void k_chain_finish(const uint64_t* __restrict__ seg_begin, const uint32_t* __restrict__ pkt_flow,
                                uint64_t n_pkts, const uint32_t* __restrict__ pseudo,
-                               const uint32_t* __restrict__ fseg, uint16_t* __restrict__ out) {
+                               const uint32_t* __restrict__ fseg, uint16_t* __restrict__ out, uint64_t n_segs,
+                               uint32_t n_flows, uint32_t* __restrict__ err) {
     const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pkts) return;
+    const uint64_t b = seg_begin[p], e = seg_begin[p + 1];
+    const uint32_t flow = pkt_flow ? pkt_flow[p] : 0u;
+    bool bad = b > e || e > n_segs || (pseudo && flow >= n_flows);
     uint32_t total_len = 0, F = 0;  // pip_buf::total_len is a u32 (pip/pip_buf.h:17)
-    for (uint64_t s = seg_begin[p], e = seg_begin[p + 1]; s < e; s++) {
+    for (uint64_t s = b; !bad && s < e; s++) {
         const uint32_t x = fseg[s];
+        if (x == kBadSeg) bad = true;  // (its error bit is set already)
         total_len += x >> 16;
         F += x & 0xFFFFu;
     }
-    const uint32_t P = pseudo ? pseudo[pkt_flow ? pkt_flow[p] : 0u] + len_term(total_len) : 0u;
+    if (bad) {
+        if (err) atomicOr(err, 1u << PIPCK_ERANGE);
+        out[p] = 0;
+        return;
+    }
+    const uint32_t P = pseudo ? pseudo[flow] + len_term(total_len) : 0u;
     out[p] = finish(P, F);
 }
 
@@ -1428,6 +1449,9 @@ struct Tune {
 static Tune g_tune;
 bool wave_arm() { return g_tune.lanes.load() == kWaveArm; }
 bool alt_schedule() { return (g_tune.flags.load() >> 28) & 1u; }
+uint32_t g_tune_flags() { return g_tune.flags.load(); }
+uint32_t g_tune_loads() { return g_tune.loads.load(); }
+std::atomic<uint32_t> g_probes{0};  // pipck_tune_probes (pipck_testing.h)
 
 // The batch kernel this thread launched last (pipck_common.hpp, PIPCK_LAUNCH).
 thread_local const void* t_last_kernel = nullptr;
@@ -1762,40 +1786,41 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
 template <bool FINAL, int U, bool PIPE, bool NT>
 static void launch_ragged_k(bool wide, uint64_t tiles, hipStream_t s, const uint8_t* a, const pipck_desc* d,
                             uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg, uint8_t* ok, uint32_t* err,
-                            uint32_t f) {
+                            uint32_t f, uint64_t ab, uint32_t nf) {
     // one tile per wave: the in-order dispatcher hands out tiles as waves finish
     // (measured best, profiles/r01_size_scan*.jsonl)
     // (runs of 2-4 consecutive tiles per wave measured 2-5 % slower,
     // profiles/r01_ragged_tpw_scan.jsonl)
     if (wide)
         PIPCK_LAUNCH((k_ragged<FINAL, U, PIPE, NT, 4>), dim3(grid_for(4, tiles, 0)),
-                           dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+                           dim3(256), 0, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
     else
         PIPCK_LAUNCH((k_ragged<FINAL, U, PIPE, NT, 1>), dim3(grid_for(1, tiles, 0)),
-                           dim3(64), 0, s, a, d, n, ps, out, fseg, ok, err, f);
+                           dim3(64), 0, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
 }
 
 template <int U, bool PIPE>
 static void launch_ragged_u(bool final_, bool nt, uint64_t tiles, hipStream_t s, const uint8_t* a,
                             const pipck_desc* d, uint64_t n, const uint32_t* ps, uint16_t* out, uint32_t* fseg,
-                            uint8_t* ok, uint32_t* err) {
+                            uint8_t* ok, uint32_t* err, uint64_t ab, uint32_t nf) {
     const uint32_t f = g_tune.flags.load();
     const bool wide = (f & kWideBlocks) != 0;
     if (final_) {
-        if (nt) launch_ragged_k<true, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
-        else launch_ragged_k<true, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
+        if (nt) launch_ragged_k<true, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
+        else launch_ragged_k<true, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
     } else {
-        if (nt) launch_ragged_k<false, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
-        else launch_ragged_k<false, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f);
+        if (nt) launch_ragged_k<false, U, PIPE, true>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
+        else launch_ragged_k<false, U, PIPE, false>(wide, tiles, s, a, d, n, ps, out, fseg, ok, err, f, ab, nf);
     }
 }
 
+// arena_bytes / n_flows bound every descriptor (UINT64_MAX / UINT32_MAX: trusted)
 static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_desc, uint64_t n,
                          const uint32_t* d_pseudo, uint16_t* d_out, uint32_t* d_fseg, uint8_t* d_ok, uint32_t* d_err,
-                         hipStream_t s) {
+                         hipStream_t s, uint64_t arena_bytes, uint32_t n_flows) {
     if (final_ && !d_fseg && g_tune.lanes.load() == kWaveArm)  // measurement arm: one packet per wave
-        return launch_wave(d_ok != nullptr, true, d_arena, 0, 0, d_desc, n, d_pseudo, 1u, nullptr, 0, d_out, d_ok, d_err,
-                           s, 0, g_tune.loads.load() ? g_tune.loads.load() : 4u);
+        return launch_wave(d_ok != nullptr, true, d_arena, 0, 0, d_desc, n, d_pseudo, n_flows, nullptr, 0, d_out, d_ok,
+                           d_err, s, 0, g_tune.loads.load() ? g_tune.loads.load() : 4u, arena_bytes);
     const uint64_t tiles = (n + 63) / 64;
     // loads_per_lane: 2/4/8/16 rows in flight on packed tiles (at most 4 on
     // others), 3/5/7/9/13/17/25/33 = ring-pipelined 2/4/6/8/12/16/24/32.
@@ -1806,18 +1831,18 @@ static int launch_ragged(bool final_, const void* d_arena, const pipck_desc* d_d
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
     switch (u) {
-        case 2: launch_ragged_u<2, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 4: launch_ragged_u<4, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 8: launch_ragged_u<8, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 16: launch_ragged_u<16, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 3: launch_ragged_u<2, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 9: launch_ragged_u<8, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 7: launch_ragged_u<6, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 13: launch_ragged_u<12, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 17: launch_ragged_u<16, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 25: launch_ragged_u<24, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        case 33: launch_ragged_u<32, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
-        default: launch_ragged_u<4, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err); break;
+        case 2: launch_ragged_u<2, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 4: launch_ragged_u<4, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 8: launch_ragged_u<8, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 16: launch_ragged_u<16, false>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 3: launch_ragged_u<2, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 9: launch_ragged_u<8, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 7: launch_ragged_u<6, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 13: launch_ragged_u<12, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 17: launch_ragged_u<16, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 25: launch_ragged_u<24, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        case 33: launch_ragged_u<32, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
+        default: launch_ragged_u<4, true>(final_, nt, tiles, s, a, d_desc, n, d_pseudo, d_out, d_fseg, d_ok, d_err, arena_bytes, n_flows); break;
     }
     PIPCK_LAUNCHED("k_ragged");
     return PIPCK_OK;
@@ -1893,13 +1918,19 @@ static int launch_packed(bool verify, const void* d_arena, uint64_t arena_bytes,
 
 int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
                      const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo, uint32_t* d_scratch,
-                     uint16_t* d_out, uint32_t* d_err, hipStream_t s) {
+                     uint16_t* d_out, uint32_t* d_err, hipStream_t s, uint64_t arena_bytes, uint32_t n_flows) {
     if (n_segs) {
-        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s);
+        int rc = launch_ragged(false, d_arena, d_segs, n_segs, nullptr, nullptr, d_scratch, nullptr, d_err, s,
+                               arena_bytes, UINT32_MAX);
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)((n_packets + 255) / 256)), dim3(256), 0, s, d_seg_begin,
-                       d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out);
+    const uint64_t blocks = (n_packets + 255) / 256;
+    if (blocks > 0x7FFFFFFFull) {
+        set_error("pipck_checksum_chains: too many packets for one launch");
+        return PIPCK_ERANGE;
+    }
+    hipLaunchKernelGGL(k_chain_finish, dim3((uint32_t)blocks), dim3(256), 0, s, d_seg_begin, d_pkt_flow, n_packets,
+                       d_pseudo, d_scratch, d_out, n_segs, n_flows, d_err);
     PIPCK_LAUNCHED("k_chain_finish");
     return PIPCK_OK;
 }
@@ -1913,7 +1944,7 @@ using namespace pipck;
 // ---------------------------------------------------------------------------
 extern "C" {
 
-uint32_t pipck_version(void) { return (1u << 16) | 0u; }
+uint32_t pipck_version(void) { return ((uint32_t)PIPCK_VERSION_MAJOR << 16) | PIPCK_VERSION_MINOR; }
 
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags) {
     g_tune.lanes.store(lanes_per_packet);
@@ -1943,6 +1974,8 @@ int pipck_last_launch(char* buf, size_t cap) {
     if (rc) set_error("pipck_last_launch: buffer too small");
     return rc;
 }
+
+void pipck_tune_probes(uint32_t probes) { g_probes.store(probes); }
 
 int pipck_tune_xcd_weights(const uint32_t* m, uint32_t period) {
     uint32_t w[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2009,24 +2042,46 @@ int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint6
                         stream);
 }
 
-int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
-                          uint16_t* d_out, uint32_t* d_err, void* stream) {
+int pipck_checksum_ragged_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_desc, uint64_t n,
+                            const uint32_t* d_pseudo, uint32_t n_flows, uint16_t* d_out, uint32_t* d_err,
+                            void* stream) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_desc || !d_out) {
         set_error("pipck_checksum_ragged: null pointer");
         return PIPCK_EINVAL;
     }
-    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, d_out, nullptr, nullptr, d_err, as_stream(stream));
+    if (d_pseudo && n_flows == 0) {
+        set_error("pipck_checksum_ragged_n: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
+    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, d_out, nullptr, nullptr, d_err, as_stream(stream),
+                         arena_bytes, n_flows);
 }
 
-int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
-                        uint8_t* d_ok, uint32_t* d_err, void* stream) {
+int pipck_verify_ragged_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_desc, uint64_t n,
+                          const uint32_t* d_pseudo, uint32_t n_flows, uint8_t* d_ok, uint32_t* d_err, void* stream) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_desc || !d_ok) {
         set_error("pipck_verify_ragged: null pointer");
         return PIPCK_EINVAL;
     }
-    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, nullptr, nullptr, d_ok, d_err, as_stream(stream));
+    if (d_pseudo && n_flows == 0) {
+        set_error("pipck_verify_ragged_n: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
+    return launch_ragged(true, d_arena, d_desc, n, d_pseudo, nullptr, nullptr, d_ok, d_err, as_stream(stream),
+                         arena_bytes, n_flows);
+}
+
+// the unbounded forms (descriptors and flows trusted)
+int pipck_checksum_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
+                          uint16_t* d_out, uint32_t* d_err, void* stream) {
+    return pipck_checksum_ragged_n(d_arena, UINT64_MAX, d_desc, n, d_pseudo, UINT32_MAX, d_out, d_err, stream);
+}
+
+int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n, const uint32_t* d_pseudo,
+                        uint8_t* d_ok, uint32_t* d_err, void* stream) {
+    return pipck_verify_ragged_n(d_arena, UINT64_MAX, d_desc, n, d_pseudo, UINT32_MAX, d_ok, d_err, stream);
 }
 
 int pipck_checksum_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
@@ -2080,16 +2135,29 @@ int pipck_packed_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_chun
     return PIPCK_OK;
 }
 
-int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
-                          const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo,
-                          uint32_t* d_scratch, uint16_t* d_out, uint32_t* d_err, void* stream) {
+int pipck_checksum_chains_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_segs, uint64_t n_segs,
+                            const uint64_t* d_seg_begin, const uint32_t* d_pkt_flow, uint64_t n_packets,
+                            const uint32_t* d_pseudo, uint32_t n_flows, uint32_t* d_scratch, uint16_t* d_out,
+                            uint32_t* d_err, void* stream) {
     if (n_packets == 0) return PIPCK_OK;
     if (!d_seg_begin || !d_out || (n_segs && (!d_arena || !d_segs || !d_scratch))) {
         set_error("pipck_checksum_chains: null pointer");
         return PIPCK_EINVAL;
     }
+    if (d_pseudo && n_flows == 0) {
+        set_error("pipck_checksum_chains_n: n_flows == 0");
+        return PIPCK_EINVAL;
+    }
     return chains_unchecked(d_arena, d_segs, n_segs, d_seg_begin, d_pkt_flow, n_packets, d_pseudo, d_scratch, d_out,
-                            d_err, as_stream(stream));
+                            d_err, as_stream(stream), arena_bytes, n_flows);
+}
+
+// segments and flows trusted (segment ranges are still bounded by n_segs)
+int pipck_checksum_chains(const void* d_arena, const pipck_desc* d_segs, uint64_t n_segs, const uint64_t* d_seg_begin,
+                          const uint32_t* d_pkt_flow, uint64_t n_packets, const uint32_t* d_pseudo,
+                          uint32_t* d_scratch, uint16_t* d_out, uint32_t* d_err, void* stream) {
+    return pipck_checksum_chains_n(d_arena, UINT64_MAX, d_segs, n_segs, d_seg_begin, d_pkt_flow, n_packets, d_pseudo,
+                                   UINT32_MAX, d_scratch, d_out, d_err, stream);
 }
 
 }  // extern "C"

@@ -40,7 +40,19 @@ namespace pipck {
 
 // ---- frames in fixed-size slots (a receive ring: slot i at arena + i * stride,
 // lens[i] bytes of frame in it, the rest of the slot unused) -----------------
-// k_ring_rx (the row stream; launch_ring_rx's default is k_ring_slots below)
+// A slot length is written by whoever filled the ring (a peer device, a NIC, a
+// tun reader: pip itself trusts the IP lengths of what recv() gave it,
+// pip/pip_netif.cpp:45-77), so every ring kernel bounds it by the slot: a slot
+// claiming more than slot_stride bytes is not read at all, gets verdict 0 and
+// sets (1 << PIPCK_ERANGE) in err -- no load, and no parse read, leaves its slot.
+//
+// Three schedules (launch_ring_rx picks; all give the same verdicts):
+//  * k_ring (the default, below k_ring_slots): slot groups, each wave choosing
+//    per its own slots' lengths;
+//  * k_ring_rx: a row stream over whole slots (tune flag bit 28);
+//  * k_ring_slots: slot by slot, a wave per slot (the wave-per-packet arm).
+//
+// k_ring_rx (the row stream)
 // streams the slots like k_flat_coop (pipck_coop.hip): a block task
 // of K whole slots, its four waves on interleaved 1 KiB rows, a ring of U rows
 // per wave, one LDS partial per lane per slot.  Unlike k_flat_coop each lane's
@@ -56,7 +68,7 @@ __host__ __device__ constexpr uint32_t ring_pitch(uint32_t k) { return k | 1u; }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_ring_rx(
     const uint8_t* __restrict__ arena, uint32_t cpp, const uint16_t* __restrict__ lens, uint64_t n, uint32_t K,
-    uint8_t* __restrict__ ok) {
+    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
     extern __shared__ uint32_t s_ring[];  // part[64][pitch] | len[K] | hdr[6][K] (u32x4), launch_ring_rx sizes it
     const uint32_t pitch = ring_pitch(K);
     uint32_t* s_part = s_ring;
@@ -68,7 +80,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)K, n - p0);
     const uint32_t rows = (np * cpp + 63u) >> 6;
     for (uint32_t i = threadIdx.x; i < 64u * pitch; i += 256) s_part[i] = 0;
-    for (uint32_t i = threadIdx.x; i < K; i += 256) s_len[i] = i < np ? (uint32_t)lens[p0 + i] : 0u;
+    for (uint32_t i = threadIdx.x; i < K; i += 256) {
+        const uint32_t L = i < np ? (uint32_t)lens[p0 + i] : 0u;
+        s_len[i] = L > 16u * cpp ? 0u : L;  // longer than its slot: not read (judged at the end)
+    }
     __syncthreads();
     const buf_t tb = buf_rsrc(arena + p0 * cpp * 16u, np * cpp * 16u);
     uint32_t* part = s_part + lane * pitch;
@@ -147,7 +162,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
         }
         const uint8_t* pkp = arena + (p0 + i) * cpp * 16u;
-        store_result8(buf_rsrc(ok + p0, np), i, rx_from_window(pkp, L, F, hw));
+        const bool bad = (uint32_t)lens[p0 + i] > 16u * cpp;
+        if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
+        store_result8(buf_rsrc(ok + p0, np), i, bad ? 0u : rx_from_window(pkp, L, F, hw));
     }
 }
 
@@ -160,12 +177,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // at once, a frame longer than 1 KiB then streams its further rows 4 at a time,
 // and one wave reduce per slot gives its sum.  Lanes 0-5 of the first row are
 // the header window; the block's 32 slots are judged by its first 32 threads.
-// The default schedule (launch_ring_rx).
+// The round-4 default, now a measurement arm (the wave-per-packet tune arm).
 constexpr int kSlotG = 8;
 
 __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ arena, uint32_t cpp,
                                                     const uint16_t* __restrict__ lens, uint64_t n,
-                                                    uint8_t* __restrict__ ok) {
+                                                    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
     __shared__ u32x4 s_hdr[6][4 * kSlotG];
     __shared__ uint32_t s_sum[4 * kSlotG], s_len[4 * kSlotG];
     const int lane = threadIdx.x & 63;
@@ -179,7 +196,7 @@ __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ 
 #pragma unroll
     for (int g = 0; g < kSlotG; g++) {
         L[g] = (uint32_t)__builtin_amdgcn_readlane((int)lmine, g);
-        Lc[g] = min(L[g], 16u * cpp);  // the slot bounds the bytes read
+        Lc[g] = L[g] > 16u * cpp ? 0u : L[g];  // longer than its slot: not read (verdict 0 below)
         r[g] = buf_rsrc(arena + (p0 + g) * cpp * 16u, (Lc[g] + 15u) & ~15u);  // slots past n: L = 0
         v[g] = buf_load<true>(r[g], (uint32_t)lane * 16u);
     }
@@ -219,12 +236,179 @@ __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ 
             hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
         }
         const uint8_t* pkp = arena + (b0 + i) * cpp * 16u;
-        store_result8(buf_rsrc(ok + b0, np), i, rx_from_window(pkp, Li, F, hw));
+        const bool bad = Li > 16u * cpp;
+        if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
+        store_result8(buf_rsrc(ok + b0, np), i, bad ? 0u : rx_from_window(pkp, Li, F, hw));
     }
 }
 
+// ---- the default: slot groups, each wave choosing its schedule ---------------
+// A wave owns W consecutive slots (W = 64 for slots up to 2 KiB, 32 up to 4 KiB,
+// 16 above: about 64-150 KiB of slot per wave task) and looks at their lengths
+// before it reads a byte (wave-uniform choice, so a ring may mix fills):
+//  * every frame <= 512 B: S lanes per slot (S = 8 / 16 / 32, the least power
+//    of two covering the longest frame in chunks), 64 / S slots per load
+//    instruction, one segmented DPP reduce per instruction -- short frames in
+//    small slots cost a few instructions per slot, not a wave reduce each
+//    (k_ring_slots: 0.62 ms for 8M ~130-B frames, all of it per-slot work);
+//  * otherwise a stream of the wave's (slot, 1 KiB row) items that hold frame
+//    bytes, U loads in flight: the rows of a slot follow each other, rows past a
+//    frame are never issued (a sparse ring costs its frame bytes), and a full
+//    ring streams like the fixed-stride kernels; a run partial per lane is
+//    flushed with one wave reduce per slot.
+// Each slot's header window (its first six chunks) goes to LDS on the way, and
+// at the end lane g judges slot g with rx_from_window from its sum and window.
+constexpr uint32_t kRingW = 64;  // slots per wave at most (one per lane at the end)
+
+struct RingLds {
+    u32x4 hdr[6][kRingW];  // chunk k of slot g's header window
+    uint32_t sum[kRingW];  // slot g's LE residue sum
+};
+
+// Sum of v over each aligned group of S lanes (S = 8, 16, 32), valid in lane
+// S / 2 of the group: two quad swaps, a half-row mirror (8), a row mirror
+// (16), then row_bcast:15 into rows 1 and 3 (32) -- DPP only, no LDS trips.
+template <int S>
+__device__ __forceinline__ uint32_t group_total(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    if (S >= 16) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);  // row_mirror
+    if (S >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    return v;
+}
+
+// Short frames: group gi = lane / S of load t takes slot t * (64 / S) + gi,
+// lane k = lane % S its chunk k.  Lc: this lane's own slot's readable bytes
+// (lane g holds slot g's), fetched per load for the group's slot.
+template <int S, int U>
+__device__ __forceinline__ void ring_short(RingLds& t, buf_t rb, uint32_t stride, uint32_t np, uint32_t Lc,
+                                           int lane) {
+    constexpr uint32_t P = 64u / S;  // slots per load
+    const uint32_t k = (uint32_t)lane % S, gi = (uint32_t)lane / S;
+    const uint32_t loads = (np + P - 1) / P;  // <= 64 / P
+    for (uint32_t t0 = 0; t0 < loads; t0 += U) {
+        u32x4 v[U];
+        uint32_t lg[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t g = (t0 + u) * P + gi;  // < 64 while t0 + u < loads
+            lg[u] = (uint32_t)__shfl((int)Lc, (int)(g & 63u), 64);
+            const bool in = t0 + u < loads && 16u * k < lg[u];
+            v[u] = buf_load<true>(rb, in ? g * stride + 16u * k : 0xFFFFFFF0u);  // past the frame: no request
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (t0 + u < loads) {  // wave-uniform
+                const uint32_t g = (t0 + u) * P + gi;
+                const int hi = (int)lg[u] - 16 * (int)k;
+                const u32x4 x = hi < 16 ? mask_tail(v[u], hi) : v[u];
+                const uint32_t tot = group_total<S>(dot4(x, 0u));
+                if (k == S / 2) t.sum[g] = tot;
+                if (k < 6) t.hdr[k][g] = x;
+            }
+        }
+    }
+}
+
+// Longer frames: item i of the wave's stream = row r of slot g, for the slots'
+// row counts R_g = ceil(chunks_g / 64) in slot order (incl = their inclusive
+// prefix, lane g).  Slot of item i: the number of slots whose rows all come
+// before it (a ballot popcount); its row: i minus the rows before the slot.
+template <int U>
+__device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride, uint32_t Lc, uint32_t R,
+                                          int lane) {
+    const uint32_t incl = wave_incl_scan(R);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // items
+    const uint32_t excl = incl - R;
+    u32x4 v[U];
+    uint32_t sg[U], sr[U], sl[U];  // per ring entry: slot, row, slot bytes (scalars)
+    auto issue = [&](uint32_t i, int u) {
+        uint32_t g = 0, r = 0, L = 0;
+        if (i < T) {  // wave-uniform
+            g = (uint32_t)__popcll(__ballot(incl <= i));
+            r = i - (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)g);
+            L = (uint32_t)__builtin_amdgcn_readlane((int)Lc, (int)g);
+        }
+        sg[u] = g, sr[u] = r, sl[u] = L;
+        const uint32_t c = 64u * r + (uint32_t)lane;
+        v[u] = buf_load<true>(rb, 16u * c < L ? g * stride + 16u * c : 0xFFFFFFF0u);
+    };
+#pragma unroll
+    for (int u = 0; u < U; u++) issue((uint32_t)u, u);
+    uint32_t cur = 0xFFFFFFFFu, acc = 0;
+    for (uint32_t j0 = 0; j0 < T; j0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = j0 + u;
+            if (i < T) {  // wave-uniform
+                const uint32_t g = sg[u], r = sr[u];
+                if (g != cur) {  // the previous slot's rows are all in: one wave reduce
+                    if (cur != 0xFFFFFFFFu) {
+                        const uint32_t s = wave_total(acc);
+                        if (lane == 0) t.sum[cur] = s;
+                    }
+                    cur = g;
+                    acc = 0;
+                }
+                const int hi = (int)sl[u] - 16 * (int)(64u * r + (uint32_t)lane);
+                const u32x4 x = hi < 16 ? mask_tail(v[u], hi) : v[u];
+                acc = dot4(x, acc);
+                if (r == 0 && lane < 6) t.hdr[lane][g] = x;
+            }
+            issue(i + U, u);  // past the stream: no request
+        }
+    }
+    if (cur != 0xFFFFFFFFu) {
+        const uint32_t s = wave_total(acc);
+        if (lane == 0) t.sum[cur] = s;
+    }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
+                                              const uint16_t* __restrict__ lens, uint64_t n, uint32_t W,
+                                              uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
+    __shared__ RingLds s_ring[4];
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    RingLds& t = s_ring[w];
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 4u + w) * W;
+    if (p0 >= n) return;  // wave-uniform
+    const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)W, n - p0);
+    const bool valid = (uint32_t)lane < np;
+    const uint32_t L = valid ? (uint32_t)lens[p0 + lane] : 0u;
+    const bool bad = L > stride;              // longer than its slot: not read, verdict 0
+    const uint32_t Lc = bad ? 0u : L;         // the bytes this slot reads
+    const uint32_t nch = (Lc + 15u) >> 4;
+    const uint32_t cmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(nch), 63);
+    const buf_t rb = buf_rsrc(arena + p0 * stride, np * stride);  // the wave's slots
+    if (cmax <= 8)
+        ring_short<8, 8>(t, rb, stride, np, Lc, lane);
+    else if (cmax <= 16)
+        ring_short<16, 16>(t, rb, stride, np, Lc, lane);
+    else if (cmax <= 32)
+        ring_short<32, 16>(t, rb, stride, np, Lc, lane);
+    else
+        ring_rows<U>(t, rb, stride, Lc, (nch + 63u) >> 6, lane);
+    wave_sync();
+    uint32_t r = 0;
+    if (valid && !bad) {
+        const uint32_t F = bswap16(fold16(nch ? t.sum[lane] : 0u));  // slots start 16-byte aligned: even address
+        uint32_t hw[24];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {  // chunks past the frame were never captured: zero
+            const u32x4 x = 16u * k < L ? t.hdr[k][lane] : u32x4{0u, 0u, 0u, 0u};
+            hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
+        }
+        r = rx_from_window(arena + (p0 + (uint32_t)lane) * stride, L, F, hw);
+    }
+    if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
+    store_result8(buf_rsrc(ok + p0, np), (uint32_t)lane, r);
+}
+
 int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
-                   hipStream_t s) {
+                   uint32_t* d_err, hipStream_t s) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_lens || !d_ok) {
         set_error("pipck_rx_verify_ring: null pointer");
@@ -236,38 +420,55 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         return PIPCK_EINVAL;
     }
     const uint32_t cpp = (uint32_t)(stride / 16);
-    // slot by slot (k_ring_slots) by default: a sparse 9,216-B ring of cfg4's
-    // Zipf frames 7.01 -> 1.33 ms, ~260-B frames in 2 KiB slots 1.90 -> 0.62,
-    // ~160-B frames in 1 KiB slots 1.80 -> 0.62; the row stream wins only on
-    // full slots (1,536-B: 0.83 against 0.73; 9,216-B: 0.87 against 0.85),
-    // profiles/r04_ring_schedule_ab.jsonl.  A ring's fill is not known at launch,
-    // and a 13 % loss on full rings weighs less than a 3-5x loss on sparse ones.
-    // pipck_tune flag bit 28 (the other schedule) selects the row stream.
-    if (wave_arm() || !alt_schedule()) {
+    const uint32_t flags = g_tune_flags();
+    if (wave_arm()) {  // measurement arm: slot by slot, a wave per slot
         const uint64_t blocks = (n + 4u * kSlotG - 1) / (4u * kSlotG);
         if (blocks > 0x7FFFFFFFull) {
             set_error("pipck_rx_verify_ring: too many slots for one launch");
             return PIPCK_ERANGE;
         }
         PIPCK_LAUNCH(k_ring_slots, dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)d_arena, cpp, d_lens, n,
-                     d_ok);
+                     d_ok, d_err);
         PIPCK_LAUNCHED("k_ring_slots");
         return PIPCK_OK;
     }
-    // K slots per block task: ~4 waves x 48 rows (x 64 for jumbo slots), a
-    // multiple of 8, at most 256 (one slot per thread at the end) -- k_flat_coop's
-    uint32_t K = (4u * (cpp >= 256 ? 64u : 48u) * 64u) / cpp;
-    K = std::max<uint32_t>(8u, std::min<uint32_t>(256u, K / 8u * 8u));
-    if ((uint64_t)K * stride >= (1ull << 31)) return PIPCK_EINVAL;
-    const uint64_t blocks = (n + K - 1) / K;
+    if (alt_schedule()) {  // measurement arm: the row stream over whole slots
+        // K slots per block task: ~4 waves x 48 rows (x 64 for jumbo slots), a
+        // multiple of 8, at most 256 (one slot per thread at the end) -- k_flat_coop's
+        uint32_t K = (4u * (cpp >= 256 ? 64u : 48u) * 64u) / cpp;
+        K = std::max<uint32_t>(8u, std::min<uint32_t>(256u, K / 8u * 8u));
+        if ((uint64_t)K * stride >= (1ull << 31)) return PIPCK_EINVAL;
+        const uint64_t blocks = (n + K - 1) / K;
+        if (blocks > 0x7FFFFFFFull) {
+            set_error("pipck_rx_verify_ring: too many slots for one launch");
+            return PIPCK_ERANGE;
+        }
+        const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
+        PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
+                     d_ok, d_err);
+        PIPCK_LAUNCHED("k_ring_rx");
+        return PIPCK_OK;
+    }
+    // slot groups (k_ring).  W slots per wave: 64 up to 2 KiB slots, 32 up to 4
+    // KiB, 16 above, or tune bits 8..15 (16 / 32 / 64); U loads in flight in the
+    // row stream: 16, or loads_per_lane 8 / 24 / 32.
+    uint32_t W = stride <= 2048 ? 64u : (stride <= 4096 ? 32u : 16u);
+    const uint32_t wt = (flags >> 8) & 0xFFu;
+    if (wt == 16 || wt == 32 || wt == 64) W = wt;
+    const uint64_t blocks = (n + 4u * W - 1) / (4u * W);
     if (blocks > 0x7FFFFFFFull) {
         set_error("pipck_rx_verify_ring: too many slots for one launch");
         return PIPCK_ERANGE;
     }
-    const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
-    PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
-                 d_ok);
-    PIPCK_LAUNCHED("k_ring_rx");
+    const uint8_t* a = (const uint8_t*)d_arena;
+    const uint32_t st = (uint32_t)stride;
+    switch (g_tune_loads()) {
+        case 8: PIPCK_LAUNCH(k_ring<8>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
+        case 24: PIPCK_LAUNCH(k_ring<24>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
+        case 32: PIPCK_LAUNCH(k_ring<32>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
+        default: PIPCK_LAUNCH(k_ring<16>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
+    }
+    PIPCK_LAUNCHED("k_ring");
     return PIPCK_OK;
 }
 
@@ -275,9 +476,15 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
 
 extern "C" {
 
+int pipck_rx_verify_ring_n(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n,
+                           uint8_t* d_ok, uint32_t* d_err, void* stream) {
+    return pipck::launch_ring_rx(d_arena, slot_stride, d_lens, n, d_ok, d_err, pipck::as_stream(stream));
+}
+
+// the same without the error word (every slot is still bounded on the device)
 int pipck_rx_verify_ring(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n,
                          uint8_t* d_ok, void* stream) {
-    return pipck::launch_ring_rx(d_arena, slot_stride, d_lens, n, d_ok, pipck::as_stream(stream));
+    return pipck_rx_verify_ring_n(d_arena, slot_stride, d_lens, n, d_ok, nullptr, stream);
 }
 
 int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,

@@ -50,7 +50,9 @@ extern "C" {
  * checksum mode, non-temporal loads, rings 24/32 for k_flat); the production
  * kernels have them compiled out and ignore them otherwise.
  * Bit 28 = the other fixed-stride schedule (and for pipck_rx_verify_ring the
- * row stream k_ring_rx instead of the default k_ring_slots): k_flat (one task per wave)
+ * row stream k_ring_rx instead of the default k_ring; lanes_per_packet = 256
+ * there selects k_ring_slots, and bits 8..15 = 16 / 32 / 64 set k_ring's slots
+ * per wave, loads_per_lane 8 / 24 / 32 its loads in flight): k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
  * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
  * for k_flat_coop, bits 8..15 are rows per wave
@@ -68,6 +70,14 @@ extern "C" {
  * result-store policy: 29 = plain write-back, 30 = non-temporal (default
  * write-through sc1), 31 = one store per result instead of 16-byte pieces. */
 void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blocks, uint32_t flags);
+
+/* MEASUREMENT-ONLY probes that CHANGE RESULTS, kept apart from pipck_tune's
+ * flags (whose settings all compute the same results; process-wide, internal).
+ * Bit 0 = k_hdr stores each IPv4 header's checksum into the header's ip_sum
+ * (htons, byte 10, as pip_netif.cpp:97 stores it) and leaves the result array
+ * untouched (the "results inside the headers" layout).
+ * 0 switches every probe off. */
+void pipck_tune_probes(uint32_t probes);
 
 /* XCD-weighted static deal for k_flat (ring 24, checksum; measurement arm,
  * VERDICT r03 item 7): the grid is cut into periods of 8 x period blocks and

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ arena,
                                               const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                               const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                              uint32_t* __restrict__ err) {
+                                              uint32_t* __restrict__ err, uint64_t arena_bytes) {
     const int lane = threadIdx.x & 63;
     const uint64_t pkt = (uint64_t)blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (pkt >= n) return;  // wave-uniform
@@ -44,8 +44,10 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ arena,
         off = first_lane_u64(d.offset);
         L = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.len);
         flow = (uint32_t)__builtin_amdgcn_readfirstlane((int)d.flow);
-        bad = L > PIPCK_MAX_SEG_LEN;
-        if (bad) L = 0;
+        // out of domain (as k_ragged): too long, past the arena, or a flow past the table
+        bad = L > PIPCK_MAX_SEG_LEN || off > arena_bytes || (uint64_t)L > arena_bytes - off ||
+              (pseudo && flow >= n_flows);
+        if (bad) L = 0, flow = 0;
     } else {
         off = pkt * stride;
         L = len;
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ arena,
 }
 
 typedef void (*wave_fn)(const uint8_t*, uint64_t, uint32_t, const pipck_desc*, uint64_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t*);
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t*, uint64_t);
 
 // loads per lane per pass: 2 for packets up to 2 KiB, 4 above (cfg3 / cfg5 at
 // 4: 0.85 / 0.84 of HBM peak against 0.71-0.73 / 0.69-0.71 at 8 and 16, which
@@ -88,7 +90,7 @@ typedef void (*wave_fn)(const uint8_t*, uint64_t, uint32_t, const pipck_desc*, u
 int launch_wave(bool verify, bool desc, const void* d_arena, uint64_t stride, uint32_t len, const pipck_desc* d_desc,
                 uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                 uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s,
-                uint32_t max_chunks, uint32_t nl) {
+                uint32_t max_chunks, uint32_t nl, uint64_t arena_bytes) {
     static const wave_fn kWave[4][2][2] = {  // [NL 2/4/8/16][verify][desc]
         {{k_wave<2, false, false>, k_wave<2, false, true>}, {k_wave<2, true, false>, k_wave<2, true, true>}},
         {{k_wave<4, false, false>, k_wave<4, false, true>}, {k_wave<4, true, false>, k_wave<4, true, true>}},
@@ -102,7 +104,7 @@ int launch_wave(bool verify, bool desc, const void* d_arena, uint64_t stride, ui
         return PIPCK_ERANGE;
     }
     PIPCK_LAUNCH(kWave[ni][verify][desc], dim3((uint32_t)blocks), dim3(256), 0, s, (const uint8_t*)d_arena, stride,
-                 len, d_desc, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, d_err);
+                 len, d_desc, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, d_err, arena_bytes);
     PIPCK_LAUNCHED("k_wave");
     return PIPCK_OK;
 }

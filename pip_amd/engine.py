@@ -107,24 +107,27 @@ def verify_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: 
 
 
 def checksum_ragged(arena, desc, pseudo=None, out=None, err=None):
-    """desc: device int64 tensor (n, 2) laid out as pipck_desc."""
+    """desc: device int64 tensor (n, 2) laid out as pipck_desc.  Bounded on the device
+    (pipck_checksum_ragged_n): a descriptor past the arena, longer than 65535 B or naming a
+    flow past `pseudo` gets 0 and ORs 1 << PIPCK_ERANGE into err (optional device int32)."""
     torch = _torch()
     n = desc.shape[0]
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
-    call("pipck_checksum_ragged", _ptr(arena), _ptr(desc), n, _ptr(pseudo), _ptr(out), _ptr(err),
-         current_stream(arena.device))
+    call("pipck_checksum_ragged_n", _ptr(arena), _nbytes(arena), _ptr(desc), n, _ptr(pseudo),
+         pseudo.numel() if pseudo is not None else 0, _ptr(out), _ptr(err), current_stream(arena.device))
     return out
 
 
 def verify_ragged(arena, desc, pseudo=None, ok=None, err=None):
-    """RX verification of a ragged batch whose packets carry their checksum field."""
+    """RX verification of a ragged batch whose packets carry their checksum field
+    (pipck_verify_ragged_n, bounded as checksum_ragged)."""
     torch = _torch()
     n = desc.shape[0]
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
-    call("pipck_verify_ragged", _ptr(arena), _ptr(desc), n, _ptr(pseudo), _ptr(ok), _ptr(err),
-         current_stream(arena.device))
+    call("pipck_verify_ragged_n", _ptr(arena), _nbytes(arena), _ptr(desc), n, _ptr(pseudo),
+         pseudo.numel() if pseudo is not None else 0, _ptr(ok), _ptr(err), current_stream(arena.device))
     return ok
 
 
@@ -234,16 +237,18 @@ def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None
     return ok
 
 
-def rx_verify_ring(ring, stride: int, lens, n: int | None = None, ok=None):
-    """Received frames in the fixed-size slots of a device ring (pipck_rx_verify_ring): the
-    PIPCK_RX_* bits per slot (uint8)."""
+def rx_verify_ring(ring, stride: int, lens, n: int | None = None, ok=None, err=None):
+    """Received frames in the fixed-size slots of a device ring (pipck_rx_verify_ring_n): the
+    PIPCK_RX_* bits per slot (uint8).  A slot length past the stride is refused on the device
+    (verdict 0, 1 << PIPCK_ERANGE OR-ed into err, an optional device int32)."""
     torch = _torch()
     n = lens.numel() if n is None else n
-    if n * stride > _nbytes(ring):
-        raise ValueError("ring smaller than n * stride")
+    if n * stride > _nbytes(ring) or n > lens.numel():
+        raise ValueError("ring smaller than n * stride, or fewer lengths than slots")
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=ring.device)
-    call("pipck_rx_verify_ring", _ptr(ring), stride, _ptr(lens), n, _ptr(ok), current_stream(ring.device))
+    call("pipck_rx_verify_ring_n", _ptr(ring), stride, _ptr(lens), n, _ptr(ok), _ptr(err),
+         current_stream(ring.device))
     return ok
 
 
@@ -271,14 +276,17 @@ def packed_bytes_index(lens, n: int | None = None):
 
 
 def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None, err=None):
-    """segs: (n_segs, 2) int64 descriptors; seg_begin: (n_packets+1,) int64 CSR offsets."""
+    """segs: (n_segs, 2) int64 descriptors; seg_begin: (n_packets+1,) int64 CSR offsets.
+    Bounded on the device (pipck_checksum_chains_n): a packet with a segment past the arena,
+    a flow past `pseudo` or a segment range outside segs gets 0 and sets err (as checksum_ragged)."""
     torch = _torch()
     n_pk = seg_begin.shape[0] - 1
     scratch = torch.empty(max(segs.shape[0], 1), dtype=torch.int32, device=arena.device)
     if out is None:
         out = torch.empty(n_pk, dtype=torch.int16, device=arena.device)
-    call("pipck_checksum_chains", _ptr(arena), _ptr(segs), segs.shape[0], _ptr(seg_begin), _ptr(pkt_flow), n_pk,
-         _ptr(pseudo), _ptr(scratch), _ptr(out), _ptr(err), current_stream(arena.device))
+    call("pipck_checksum_chains_n", _ptr(arena), _nbytes(arena), _ptr(segs), segs.shape[0], _ptr(seg_begin),
+         _ptr(pkt_flow), n_pk, _ptr(pseudo), pseudo.numel() if pseudo is not None else 0, _ptr(scratch), _ptr(out),
+         _ptr(err), current_stream(arena.device))
     return out
 
 
@@ -478,7 +486,8 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
     except the measurement-only probes loads_only (bit 21), no_task_end (22), end_no_store (23) and
-    hdr_in_place (bit 28 read by k_hdr: results into the headers' ip_sum, the result array untouched)."""
+    hdr_in_place (pipck_tune_probes bit 0, not a tune flag: k_hdr stores the results into the headers'
+    ip_sum and leaves the result array untouched).  alt_flat_schedule (bit 28) never changes results."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
@@ -486,7 +495,8 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (0 if flat_small else 128) | (rows_per_task << 8) | (0 if tiny_tiles else 1 << 16)
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
              | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0) | (1 << 22 if no_task_end else 0)
-             | (1 << 23 if end_no_store else 0) | (1 << 28 if (alt_flat_schedule or hdr_in_place) else 0)
+             | (1 << 23 if end_no_store else 0) | (1 << 28 if alt_flat_schedule else 0)
              | (1 << 29 if plain_result_stores else 0) | (1 << 30 if (wave_stores or packed_no_align) else 0)
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
+    load().pipck_tune_probes(1 if hdr_in_place else 0)

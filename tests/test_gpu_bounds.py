@@ -87,3 +87,220 @@ def test_index_past_the_arena_is_an_error_not_a_fault(layout, verify):
     got, err = _run(fn, arena, nbytes, lens2, index, n, pseudo, verify)
     assert err == ERANGE_BIT and (got[64 * 40:] == 0).all()
     assert np.array_equal(got[:64 * 40], good[:64 * 40])
+
+
+# ---------------------------------------------------------------------------
+# the ring, ragged and chain ABIs bound their indices too
+# ---------------------------------------------------------------------------
+def _hip():
+    return C.CDLL("libamdhip64.so")
+
+
+class _ExactBuffer:
+    """Device memory from hipMalloc of exactly `size` bytes (no caching-allocator
+    slack after it), filled from host bytes."""
+
+    def __init__(self, data: bytes):
+        self.hip = _hip()
+        self.ptr = C.c_void_p()
+        assert self.hip.hipMalloc(C.byref(self.ptr), C.c_size_t(len(data))) == 0
+        assert self.hip.hipMemcpy(self.ptr, C.c_char_p(data), C.c_size_t(len(data)), 1) == 0  # H2D
+
+    def free(self):
+        self.hip.hipFree(self.ptr)
+
+
+def _ipv4_frame(oracle, rng, l4len, k, total_override=None):
+    from tests.test_boundary import _rx_packet
+
+    p = bytearray(_rx_packet(oracle, rng, 4, 6, l4len, k))
+    if total_override is not None:
+        p[2], p[3] = total_override >> 8, total_override & 0xFF
+    return bytes(p)
+
+
+@pytest.mark.parametrize("schedule", ["groups", "rows", "slots"])
+@pytest.mark.parametrize("stride", [1024, 9216])
+def test_ring_length_past_the_slot_is_an_error_not_a_fault(oracle, schedule, stride):
+    """pipck_rx_verify_ring_n through ctypes, no Python guard, on a ring hipMalloc'd
+    as exactly n * stride bytes: the LAST slot claims 65,535 B and carries an IPv4
+    total length past the slot; a middle slot claims stride + 16 B over a frame that
+    would verify; another claims exactly the stride (allowed).  The two refused slots
+    get verdict 0 and d_err = 1 << PIPCK_ERANGE; every other slot equals the host
+    path (pipck_rx_verify) on the same bytes, under each of the ring's schedules."""
+    import random
+
+    from tests.test_gpu_rx import RING_KERNELS, _host_bits, _last_kernel, _ring_frames, _ring_schedule
+
+    rng = random.Random(stride + 99)
+    n = 256 + 77  # several waves / blocks of every schedule, the last one partial
+    frames = _ring_frames(oracle, rng, stride, "short" if stride == 1024 else "mixed", n)
+    full = _ipv4_frame(oracle, rng, stride - 20, 5)  # exactly one slot
+    frames[100] = full
+    frames[n - 1] = _ipv4_frame(oracle, rng, 400, 7, total_override=stride + 500)  # IP total past the slot
+    frames[n - 2] = _ipv4_frame(oracle, rng, 300, 8)
+    host = _host_bits(frames)
+    blob = bytearray(n * stride)
+    for i, f in enumerate(frames):
+        blob[i * stride:i * stride + len(f)] = f
+    lens = np.array([len(f) for f in frames], dtype=np.uint16)
+    lens[n - 1] = 65535          # the last slot: far past the slot (and the ring)
+    lens[40] = stride + 16       # a middle slot: into the next slot
+    ring = _ExactBuffer(bytes(blob))
+    try:
+        dl = torch.from_numpy(lens.view(np.int16)).to("cuda")
+        ok = torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        lib = _lib.load()
+        _ring_schedule(schedule)
+        try:
+            rc = lib.pipck_rx_verify_ring_n(ring.ptr, C.c_uint64(stride), _p(dl), C.c_uint64(n), _p(ok), _p(err),
+                                            C.c_void_p(0))
+            assert rc == 0, lib.pipck_last_error()
+            torch.cuda.synchronize()
+            assert RING_KERNELS[schedule] in _last_kernel()
+        finally:
+            engine.tune()
+        got = ok.cpu().numpy()
+        assert int(err.item()) == ERANGE_BIT
+        assert got[n - 1] == 0 and got[40] == 0
+        keep = np.ones(n, dtype=bool)
+        keep[[40, n - 1]] = False
+        bad = np.nonzero(got[keep] != host[keep])[0]
+        assert bad.size == 0, bad[:5]
+        assert host[100] == 7 and got[100] == 7  # a frame filling its slot exactly is judged normally
+        # the untampered lengths: nothing refused, the middle slot judged again
+        lens_ok = np.array([len(f) for f in frames], dtype=np.uint16)
+        err.zero_()
+        rc = lib.pipck_rx_verify_ring_n(ring.ptr, C.c_uint64(stride),
+                                        _p(torch.from_numpy(lens_ok.view(np.int16)).to("cuda")), C.c_uint64(n), _p(ok),
+                                        _p(err), C.c_void_p(0))
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert int(err.item()) == 0 and np.array_equal(ok.cpu().numpy(), host)
+    finally:
+        ring.free()
+
+
+def _ragged_case(n_flows=8):
+    rng = np.random.default_rng(123)
+    size = 300_000
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = torch.from_numpy(host).to("cuda")
+    n = 64 * 5 + 9
+    offs = rng.integers(0, size - 9000, n).astype(np.uint64)
+    lens = rng.integers(0, 9000, n).astype(np.uint32)
+    flows = rng.integers(0, n_flows, n).astype(np.uint32)
+    return host, arena, offs, lens, flows
+
+
+def _tamper(offs, lens, flows, size, n_flows):
+    offs, lens, flows = offs.copy(), lens.copy(), flows.copy()
+    bad = {3: "far", 70: "straddles", 71: "overflow", 150: "flow", 200: "ends_exactly", 330: "len0_past"}
+    offs[3] = size * 100
+    offs[70], lens[70] = size - 10, 20
+    offs[71], lens[71] = (1 << 64) - 8, 64
+    flows[150] = n_flows + 3
+    offs[200], lens[200] = size - 64, 64  # ends exactly at the arena's end: allowed
+    offs[330], lens[330] = size + 1, 0     # empty, but past the end
+    refused = [i for i, why in bad.items() if why != "ends_exactly"]
+    return offs, lens, flows, refused
+
+
+@pytest.mark.parametrize("arm", ["default", "wave"])
+@pytest.mark.parametrize("verify", [False, True])
+def test_ragged_descriptor_past_the_arena_is_an_error_not_a_fault(oracle, verify, arm):
+    """pipck_{checksum,verify}_ragged_n through ctypes: descriptors far past the
+    arena, straddling its end, overflowing offset + len, naming a flow past the
+    table, or empty past the end are not read -- result 0 (verify 0), d_err =
+    1 << PIPCK_ERANGE -- while every other descriptor's result equals the
+    untampered call's, under the default kernel and the wave-per-packet arm."""
+    n_flows = 8
+    host, arena, offs, lens, flows = _ragged_case(n_flows)
+    size = host.size
+    _, pseudo = engine.gen_flows(4, n_flows, 77, 6)
+    lib = _lib.load()
+    fn = "pipck_verify_ragged_n" if verify else "pipck_checksum_ragged_n"
+
+    def run(o, ln, fl):
+        desc = engine.make_desc(o, ln, fl)
+        out = torch.zeros(len(o), dtype=torch.uint8 if verify else torch.int16, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        rc = getattr(lib, fn)(_p(arena), C.c_uint64(size), _p(desc), C.c_uint64(len(o)), _p(pseudo),
+                              C.c_uint32(n_flows), _p(out), _p(err), C.c_void_p(0))
+        torch.cuda.synchronize()
+        assert rc == 0, lib.pipck_last_error()
+        return out.cpu().numpy().view(np.uint8 if verify else np.uint16), int(err.item())
+
+    if arm == "wave":
+        engine.tune(lanes_per_packet=256)
+    try:
+        good, err0 = run(offs, lens, flows)
+        assert err0 == 0
+        o2, l2, f2, refused = _tamper(offs, lens, flows, size, n_flows)
+        # the reference results of the tampered-but-legal descriptor (200)
+        ref, _ = run(o2[[200]], l2[[200]], f2[[200]])
+        got, err = run(o2, l2, f2)
+    finally:
+        engine.tune()
+    assert err == ERANGE_BIT
+    assert (got[refused] == 0).all()
+    same = np.setdiff1d(np.arange(len(offs)), refused + [200])
+    assert np.array_equal(got[same], good[same])
+    assert got[200] == ref[0]
+    if not verify:  # the oracle agrees on a sample (pip_inet_checksum with the flow's pseudo-header)
+        seg = host[int(o2[200]):int(o2[200]) + int(l2[200])].tobytes()
+        s, d = oracle.flow4(77, int(f2[200]))
+        assert got[200] == oracle.inet_checksum(seg, 6, s, d)
+
+
+def test_chains_bounded_by_arena_segments_and_flows(oracle):
+    """pipck_checksum_chains_n through ctypes: a packet holding one segment past the
+    arena, a packet whose segment range runs past n_segs, one whose range is
+    reversed, and one whose flow is past the table get 0 and set d_err; every
+    other packet equals the oracle's pip_inet_checksum_buf."""
+    rng = np.random.default_rng(5)
+    n_pk, n_flows, seed, proto = 300, 8, 4242, 6
+    seg_lens, seg_begin = [], [0]
+    for _ in range(n_pk):
+        seg_lens += [int(rng.integers(0, 1500)) for _ in range(int(rng.integers(1, 5)))]
+        seg_begin.append(len(seg_lens))
+    seg_lens = np.array(seg_lens, dtype=np.uint32)
+    offs = np.zeros(len(seg_lens), dtype=np.uint64)
+    pos = 0
+    for i, L in enumerate(seg_lens):
+        offs[i] = pos
+        pos += int(L) + int(rng.integers(0, 9))
+    host = rng.integers(0, 256, pos, dtype=np.uint8)
+    arena = torch.from_numpy(host).to("cuda")
+    _, pseudo = engine.gen_flows(4, n_flows, seed, proto)
+    pkt_flow = rng.integers(0, n_flows, n_pk).astype(np.int32)
+    # tamper: packet 10's second segment past the arena, packet 50's flow, packets
+    # 120 (range past n_segs) and 121 (reversed range) -- the last packet ranges kept legal
+    n_segs = len(seg_lens)
+    offs[seg_begin[10] + 1 if seg_begin[11] - seg_begin[10] > 1 else seg_begin[10]] = pos + 5000
+    pkt_flow[50] = n_flows
+    sb = np.array(seg_begin, dtype=np.int64)
+    sb_bad = sb.copy()
+    sb_bad[121] = n_segs + 40  # packet 120: [sb[120], n_segs + 40) passes n_segs; packet 121: reversed
+    refused = [10, 50, 120, 121]
+    segs = engine.make_desc(offs, seg_lens, np.zeros(n_segs))
+    scratch = torch.empty(n_segs, dtype=torch.int32, device="cuda")
+    out = torch.zeros(n_pk, dtype=torch.int16, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    lib = _lib.load()
+    rc = lib.pipck_checksum_chains_n(_p(arena), C.c_uint64(host.size), _p(segs), C.c_uint64(n_segs),
+                                     _p(torch.from_numpy(sb_bad).to("cuda")),
+                                     _p(torch.from_numpy(pkt_flow).to("cuda")), C.c_uint64(n_pk), _p(pseudo),
+                                     C.c_uint32(n_flows), _p(scratch), _p(out), _p(err), C.c_void_p(0))
+    torch.cuda.synchronize()
+    assert rc == 0, lib.pipck_last_error()
+    got = out.cpu().numpy().view(np.uint16)
+    assert int(err.item()) == ERANGE_BIT
+    assert (got[refused] == 0).all()
+    for p in range(n_pk):
+        if p in refused:
+            continue
+        chain = [host[int(offs[s]):int(offs[s]) + int(seg_lens[s])].tobytes() for s in range(sb[p], sb[p + 1])]
+        s, d = oracle.flow4(seed, int(pkt_flow[p]))
+        assert got[p] == oracle.inet_checksum_chain(chain, proto, s, d), p

@@ -414,43 +414,74 @@ def _ring(frames, stride):
     return torch.from_numpy(buf).to("cuda"), lens
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("slots", [False, True], ids=["rows", "slots"])
-@pytest.mark.parametrize("stride", [1024, 2048, 9216])
-def test_rx_verify_ring_equals_host_path(oracle, stride, slots):
-    """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
-    rest of each slot never read) gives pipck_rx_verify's bits: oracle-checksummed
-    IPv4/IPv6 TCP/UDP/ICMP frames with damage and link padding, edge frames
-    (empty, short, malformed, extension headers past the register window), every
-    frame that fits the slot."""
+# pipck_rx_verify_ring's three schedules (pipck_rxdev.hip): the default slot
+# groups (k_ring), the row stream (k_ring_rx, tune flag bit 28) and slot by slot
+# (k_ring_slots, the wave-per-packet arm)
+RING_KERNELS = {"groups": "k_ring<", "rows": "k_ring_rx", "slots": "k_ring_slots"}
+
+
+def _ring_schedule(name):
     from pip_amd import engine
 
-    rng = random.Random(stride)
+    if name == "rows":
+        engine.tune(alt_flat_schedule=True)
+    elif name == "slots":
+        engine.tune(lanes_per_packet=256)
+    else:
+        engine.tune()
+
+
+def _ring_frames(oracle, rng, stride, fill, count):
+    """count oracle-checksummed IPv4/IPv6 TCP/UDP/ICMP frames that fit the slot,
+    every third damaged, some with link padding.  fill "mixed": L4 lengths up to
+    the slot; "short": frames in runs of 16 whose longest is <= 128 / 256 / 512
+    bytes or up to the slot, so k_ring's waves take every schedule (S = 8, 16, 32
+    lanes per slot, and the row stream)."""
     frames = []
-    for k in range(3000):
+    for k in range(count):
         fam = rng.choice([4, 6])
         proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
-        l4len = rng.randint(20, min(9000, stride - 80))
+        hl = 20 if fam == 4 else 40
+        cap = stride if fill == "mixed" else (128, 256, 512, stride)[(k // 16) % 4]
+        l4len = rng.randint(20, min(9000, cap - hl - 7))
         p = bytearray(_rx_packet(oracle, rng, fam, proto, l4len, k + 1))
         if k % 3 == 1:
             p[rng.randrange(len(p))] ^= 0x04
         frames.append(bytes(p) + rng.randbytes(rng.choice([0, 0, 7])))
-    frames += [b"", bytes(10), bytes([0x45]) + bytes(30), _rx_packet(oracle, rng, 4, 1, 8, 9),
-               _rx_packet(oracle, rng, 6, 17, 300, 2, ext=_ext([(0, 20), (60, 3)], 17))]
-    frames = [f for f in frames if len(f) <= stride]
+    return frames
+
+
+def _host_bits(frames):
     lib, q = _rxq()
     try:
         bufs = [C.create_string_buffer(f, max(len(f), 1)) for f in frames]
-        host = _run(lib, q, [C.cast(b, C.c_void_p).value for b in bufs], [len(f) for f in frames])
+        return _run(lib, q, [C.cast(b, C.c_void_p).value for b in bufs], [len(f) for f in frames])
     finally:
         lib.pipck_rxq_destroy(q)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fill", ["mixed", "short"])
+@pytest.mark.parametrize("schedule", ["groups", "rows", "slots"])
+@pytest.mark.parametrize("stride", [1024, 2048, 9216])
+def test_rx_verify_ring_equals_host_path(oracle, stride, schedule, fill):
+    """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
+    rest of each slot never read) gives pipck_rx_verify's bits under each of its
+    schedules: oracle-checksummed IPv4/IPv6 TCP/UDP/ICMP frames with damage and
+    link padding, edge frames (empty, short, malformed, extension headers past
+    the register window)."""
+    from pip_amd import engine
+
+    rng = random.Random(stride * 3 + len(fill))
+    frames = _ring_frames(oracle, rng, stride, fill, 3000)
+    frames += [b"", bytes(10), bytes([0x45]) + bytes(30), _rx_packet(oracle, rng, 4, 1, 8, 9),
+               _rx_packet(oracle, rng, 6, 17, 300, 2, ext=_ext([(0, 20), (60, 3)], 17))]
+    host = _host_bits(frames)
     ring, lens = _ring(frames, stride)
-    # both schedules: the row stream (k_ring_rx) and slot by slot (k_ring_slots,
-    # the wave-per-packet arm)
-    engine.tune(lanes_per_packet=256) if slots else engine.tune(alt_flat_schedule=True)
+    _ring_schedule(schedule)
     try:
         dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
-        assert ("k_ring_slots" if slots else "k_ring_rx") in _last_kernel()
+        assert RING_KERNELS[schedule] in _last_kernel()
     finally:
         engine.tune()
     bad = np.nonzero(dev != host)[0]
@@ -467,8 +498,8 @@ def _last_kernel():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("slots", [False, True], ids=["rows", "slots"])
-def test_rx_verify_ring_full_size(slots):
+@pytest.mark.parametrize("schedule", ["groups", "rows", "slots"])
+def test_rx_verify_ring_full_size(schedule):
     """2M Zipf frames (engine.gen_rx_frames, checksummed by the ragged kernel) in
     9,216-byte slots: every frame verifies but the zero-checksum UDP ones, and the
     ring's verdicts equal the byte-packed path's on the same frames."""
@@ -478,9 +509,10 @@ def test_rx_verify_ring_full_size(slots):
 
     n, stride = 2 << 20, 9216
     ring, lens, kind = engine.gen_rx_ring(n, 31, stride)
-    engine.tune(lanes_per_packet=256) if slots else engine.tune(alt_flat_schedule=True)
+    _ring_schedule(schedule)
     try:
         ok = engine.rx_verify_ring(ring, stride, lens)
+        assert RING_KERNELS[schedule] in _last_kernel()
     finally:
         engine.tune()
     arena, lens2, tile_off, _, _, _ = engine.gen_rx_frames(n, 31)
@@ -491,11 +523,38 @@ def test_rx_verify_ring_full_size(slots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stride,l4_len", [(1024, 100), (2048, 200), (1536, 1480), (9216, 8900)])
+def test_rx_verify_ring_dense_and_short_full_size(stride, l4_len):
+    """The bench rings (tools/rx_device_bench.py) at 1M slots: short frames in small
+    slots and full slots, under all three schedules -- identical verdicts, every
+    frame verified but zero-checksum UDP."""
+    import torch
+
+    from pip_amd import engine
+
+    n = 1 << 20
+    ring, lens, kind = engine.gen_rx_ring(n, 5, stride, l4_len=l4_len)
+    got = {}
+    for schedule in RING_KERNELS:
+        _ring_schedule(schedule)
+        try:
+            got[schedule] = engine.rx_verify_ring(ring, stride, lens).clone()
+            assert RING_KERNELS[schedule] in _last_kernel()
+        finally:
+            engine.tune()
+    assert torch.equal(got["groups"], got["rows"]) and torch.equal(got["groups"], got["slots"])
+    ok = got["groups"]
+    n_ok = int((ok == VERIFIED).sum().item())
+    assert n_ok > n - 1000 and int((ok == UNCHECKED).sum().item()) == n - n_ok
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("stride", [1024, 2048, 4080, 4096, 9216])
 def test_rx_verify_ring_default_schedule(oracle, stride):
-    """The ring's default schedule (slot by slot, k_ring_slots, at every slot
-    size), and its verdicts equal the row stream's on the same ring: 1,000 oracle-checksummed frames, a third damaged, n not a multiple of
-    the 32 slots of a k_ring_slots block."""
+    """The ring's default schedule is the slot groups (k_ring) at every slot size,
+    and its verdicts equal the other two schedules' on the same ring: 1,001
+    oracle-checksummed frames, a third damaged, n not a multiple of any wave's
+    slots."""
     from pip_amd import engine
 
     rng = random.Random(stride + 7)
@@ -508,12 +567,13 @@ def test_rx_verify_ring_default_schedule(oracle, stride):
         frames.append(bytes(p))
     ring, lens = _ring(frames, stride)
     dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
-    assert "k_ring_slots" in _last_kernel()
-    engine.tune(alt_flat_schedule=True)
-    try:
-        other = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
-        assert "k_ring_rx" in _last_kernel()
-    finally:
-        engine.tune()
-    assert np.array_equal(dev, other)
+    assert "k_ring<" in _last_kernel()
+    for schedule in ("rows", "slots"):
+        _ring_schedule(schedule)
+        try:
+            other = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
+            assert RING_KERNELS[schedule] in _last_kernel()
+        finally:
+            engine.tune()
+        assert np.array_equal(dev, other), schedule
     assert 600 < int((dev == VERIFIED).sum()) < 700
