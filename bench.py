@@ -79,6 +79,9 @@ def parse(argv=None):
                         "the line then names it in config.tune_override")
     p.add_argument("--start-skew-ms", type=float, default=0.0,
                    help="rehearsal/test only: rank r waits r x this after the barrier before its timed start")
+    p.add_argument("--digest", action="store_true",
+                   help="add per_rank_results: each rank's shard (first packet id, count) and the sha256 of its "
+                        "u16 results, after the timed region (multi-rank rehearsals compare them with one-rank runs)")
     p.add_argument("--share-gpus", action="store_true",
                    help="allow more ranks than visible GPUs (ranks then share devices; rehearsal only)")
     return p.parse_args(argv)
@@ -232,6 +235,13 @@ def run_rank(args) -> int:
     ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), (t1 - t0) / 1e9, launch_s])
     clocks = shard.gather_ints(env, [t0, t1])
     placements = shard.gather_objects(env, placement)
+    digests = None
+    if args.digest:  # after the timed region: the results of this rank's shard
+        import hashlib
+
+        res = out.cpu().numpy().tobytes()
+        digests = shard.gather_objects(env, {"rank": env.rank, "first": int(first), "count": int(count),
+                                             "sha256": hashlib.sha256(res).hexdigest()})
     total_bytes = sum(r[0] for r in ranks)
     total_pkts = sum(r[1] for r in ranks)
     one_host = len({p["host"] for p in placements}) == 1
@@ -325,6 +335,8 @@ def run_rank(args) -> int:
         },
         "cpu_baseline": None,
     }
+    if digests is not None:
+        line["per_rank_results"] = digests
     if launch_bound:
         # sub-50 us launches: the event pair and launch cost as much as the kernel;
         # the rocprof trace of the same kernel and build is the kernel's own duration

@@ -120,11 +120,21 @@ bool pip_checksum_amd_capturing();
 // (pipck_host_rx_verify_packed) -- same bits; the call returns when every
 // result is known.  Returns the number of packets with ok == PIP_RX_VERIFIED.  Uses its
 // own queue: pip's deferred TX batch is not touched.
+//
+// The meaning of ok[] changed once, in place (round 4): in RX ABI 1 a verified
+// packet read ok == 3 and the return value counted those; since RX ABI 2 a
+// verified packet reads 7 and 3 means NOT checked.  Code written for ABI 1
+// would reject every verified packet and accept exactly the unchecked ones, so
+// a caller checks the ABI it compiled against (PIP_CHECKSUM_AMD_RX_ABI) and the
+// one the loaded library implements (pip_checksum_amd_rx_abi()) -- INTEGRATION.md
+// "Migration notes".
+#define PIP_CHECKSUM_AMD_RX_ABI 2
 #define PIP_RX_IP_OK 1u
 #define PIP_RX_L4_OK 2u
 #define PIP_RX_L4_CHECKED 4u
 #define PIP_RX_VERIFIED 7u
 extern "C" uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n,
                                                     uint8_t* ok);
+extern "C" uint32_t pip_checksum_amd_rx_abi(void);  // PIP_CHECKSUM_AMD_RX_ABI of the loaded library
 
 #endif

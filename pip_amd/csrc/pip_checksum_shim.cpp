@@ -266,6 +266,8 @@ pipck_rxq* rx_queue() {
 
 }  // namespace
 
+uint32_t pip_checksum_amd_rx_abi(void) { return PIP_CHECKSUM_AMD_RX_ABI; }
+
 uint32_t pip_checksum_amd_verify_packets(const void* const* pkts, const uint32_t* lens, uint32_t n, uint8_t* ok) {
     if (!n) return 0;
     if (!pkts || !lens || !ok) die("pip_checksum_amd_verify_packets: null argument", PIPCK_EINVAL);

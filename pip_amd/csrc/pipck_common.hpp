@@ -106,6 +106,7 @@ bool wave_arm();  // pipck_tune(kWaveArm, ...) is in force (pipck_kernels.hip)
 bool alt_schedule();  // pipck_tune flag bit 28 (the other schedule) is set
 uint32_t g_tune_flags();  // pipck_tune's flags / loads_per_lane in force
 uint32_t g_tune_loads();
+uint32_t g_tune_blocks();
 // measurement-only probes that change results (pipck_tune_probes, pipck_testing.h)
 constexpr uint32_t kProbeHdrInPlace = 1u;
 extern std::atomic<uint32_t> g_probes;

@@ -748,6 +748,20 @@ int pipck_host_unregister(void* p) {
 
 namespace {
 
+// Waits for both of the context's streams when a chunked host call leaves
+// early: chunks already queued may still read the caller's input by DMA and
+// write its result array, which the caller owns again once the call returns.
+struct DrainOnError {
+    pipck_ctx* c;
+    bool armed = true;
+    ~DrainOnError() {
+        if (armed) {
+            (void)hipStreamSynchronize(c->stream[0]);
+            (void)hipStreamSynchronize(c->stream[1]);
+        }
+    }
+};
+
 // Byte-packed host batches (packet i's h_lens[i] bytes right after packet
 // i-1's): chunks of whole packets, ~64 MiB of bytes (at most 1M packets) each,
 // double-buffered over the context's two streams -- H2D of the chunk's bytes
@@ -775,6 +789,7 @@ int host_packed_chunks(pipck_ctx* c, const void* h_arena, const uint16_t* h_lens
     }
     const uint8_t* src = (const uint8_t*)h_arena;
     uint64_t first = 0, off = 0;
+    DrainOnError drain{c};  // from the first enqueue on, every return waits for both streams
     for (uint64_t k = 0; first < n; k++) {
         uint64_t m = 0, bytes = 0;
         while (first + m < n && m < kMaxPkts && bytes < kTarget) bytes += h_lens[first + m++];
@@ -787,6 +802,7 @@ int host_packed_chunks(pipck_ctx* c, const void* h_arena, const uint16_t* h_lens
         first += m;
         off += bytes;
     }
+    drain.armed = false;
     PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
     PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
     return PIPCK_OK;
@@ -891,6 +907,7 @@ int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride
     const uint64_t per_chunk = std::max<uint64_t>(1, (64ull << 20) / stride);
     const size_t chunk_bytes = (size_t)(per_chunk * stride);
     if ((rc = reserve_chunks(c, chunk_bytes, per_chunk))) return rc;
+    DrainOnError drain{c};  // from the first enqueue on, every return waits for both streams
     for (uint64_t first = 0, k = 0; first < n; first += per_chunk, k++) {
         const uint64_t m = std::min<uint64_t>(per_chunk, n - first);
         const int b = (int)(k & 1);
@@ -903,6 +920,7 @@ int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride
         if (rc) return rc;
         PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
     }
+    drain.armed = false;
     PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
     PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
     return PIPCK_OK;

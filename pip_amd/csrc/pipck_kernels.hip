@@ -1451,6 +1451,7 @@ bool wave_arm() { return g_tune.lanes.load() == kWaveArm; }
 bool alt_schedule() { return (g_tune.flags.load() >> 28) & 1u; }
 uint32_t g_tune_flags() { return g_tune.flags.load(); }
 uint32_t g_tune_loads() { return g_tune.loads.load(); }
+uint32_t g_tune_blocks() { return g_tune.blocks.load(); }
 std::atomic<uint32_t> g_probes{0};  // pipck_tune_probes (pipck_testing.h)
 
 // The batch kernel this thread launched last (pipck_common.hpp, PIPCK_LAUNCH).

@@ -242,27 +242,34 @@ __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ 
     }
 }
 
-// ---- the default: slot groups, each wave choosing its schedule ---------------
-// A wave owns W consecutive slots (W = 64 for slots up to 2 KiB, 32 up to 4 KiB,
-// 16 above: about 64-150 KiB of slot per wave task) and looks at their lengths
-// before it reads a byte (wave-uniform choice, so a ring may mix fills):
+// ---- the default: slot groups of 64, the block choosing its schedule -------
+// A block of four waves owns 64 consecutive slots; every wave reads their 64
+// lengths (lane g: slot g) and the block picks its schedule from them before it
+// reads a frame byte (block-uniform, so a ring may mix fills):
 //  * every frame <= 512 B: S lanes per slot (S = 8 / 16 / 32, the least power
 //    of two covering the longest frame in chunks), 64 / S slots per load
-//    instruction, one segmented DPP reduce per instruction -- short frames in
-//    small slots cost a few instructions per slot, not a wave reduce each
-//    (k_ring_slots: 0.62 ms for 8M ~130-B frames, all of it per-slot work);
-//  * otherwise a stream of the wave's (slot, 1 KiB row) items that hold frame
-//    bytes, U loads in flight: the rows of a slot follow each other, rows past a
-//    frame are never issued (a sparse ring costs its frame bytes), and a full
-//    ring streams like the fixed-stride kernels; a run partial per lane is
-//    flushed with one wave reduce per slot.
-// Each slot's header window (its first six chunks) goes to LDS on the way, and
-// at the end lane g judges slot g with rx_from_window from its sum and window.
-constexpr uint32_t kRingW = 64;  // slots per wave at most (one per lane at the end)
+//    instruction, one segmented DPP reduce per instruction, the block's loads
+//    dealt round-robin to its waves -- short frames in small slots cost a few
+//    instructions per slot, not a wave reduce each (k_ring_slots: 0.62 ms for
+//    8M ~130-B frames, all of it per-slot work);
+//  * otherwise a stream of the block's (slot, 1 KiB row) items that hold frame
+//    bytes: rows past a frame are never issued (a sparse ring costs its frame
+//    bytes), U loads in flight per wave, a run partial per lane flushed with one
+//    wave reduce when the slot changes.  Jumbo slots (>= kRingCoopRows rows
+//    per slot on average) deal the items round-robin to the four waves, so the
+//    block reads one contiguous window (k_flat_coop's lesson); shorter ones
+//    give each wave the items of its own 16 slots.
+// Each slot's header window (its first six chunks) goes to LDS on the way; after
+// the block's barrier wave 0 judges the 64 slots (lane g: slot g) with
+// rx_from_window, so one wave's parse is spread over 64 slots.
+constexpr uint32_t kRingB = 64;               // slots per block
+constexpr uint32_t kRingCoopRows = 4;         // mean rows per slot from which the waves interleave
+constexpr uint32_t kRingOwnSlots = 1u << 29;  // pipck_tune flag (ring only): never interleave
+constexpr uint32_t kRingAllCoop = 1u << 27;   // pipck_tune flag (ring only): always interleave
 
 struct RingLds {
-    u32x4 hdr[6][kRingW];  // chunk k of slot g's header window
-    uint32_t sum[kRingW];  // slot g's LE residue sum
+    u32x4 hdr[6][kRingB];  // chunk k of slot g's header window
+    uint32_t sum[kRingB];  // slot g's LE residue sum
 };
 
 // Sum of v over each aligned group of S lanes (S = 8, 16, 32), valid in lane
@@ -278,54 +285,61 @@ __device__ __forceinline__ uint32_t group_total(uint32_t v) {
     return v;
 }
 
-// Short frames: group gi = lane / S of load t takes slot t * (64 / S) + gi,
-// lane k = lane % S its chunk k.  Lc: this lane's own slot's readable bytes
-// (lane g holds slot g's), fetched per load for the group's slot.
+// Short frames: group gi = lane / S of load j takes slot j * (64 / S) + gi,
+// lane k = lane % S its chunk k; this wave takes loads first, first + step, ...
+// Lc: lane g holds slot g's readable bytes, fetched per load for the group's
+// slot (a ds_bpermute, again at the reduce rather than held: registers set the
+// wave count, and a ring of U loads is reloaded as it is consumed).
 template <int S, int U>
-__device__ __forceinline__ void ring_short(RingLds& t, buf_t rb, uint32_t stride, uint32_t np, uint32_t Lc,
-                                           int lane) {
+__device__ __forceinline__ void ring_short(RingLds& t, buf_t rb, uint32_t stride, uint32_t nb, uint32_t Lc,
+                                           uint32_t first, uint32_t step, int lane) {
     constexpr uint32_t P = 64u / S;  // slots per load
     const uint32_t k = (uint32_t)lane % S, gi = (uint32_t)lane / S;
-    const uint32_t loads = (np + P - 1) / P;  // <= 64 / P
-    for (uint32_t t0 = 0; t0 < loads; t0 += U) {
-        u32x4 v[U];
-        uint32_t lg[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t g = (t0 + u) * P + gi;  // < 64 while t0 + u < loads
-            lg[u] = (uint32_t)__shfl((int)Lc, (int)(g & 63u), 64);
-            const bool in = t0 + u < loads && 16u * k < lg[u];
-            v[u] = buf_load<true>(rb, in ? g * stride + 16u * k : 0xFFFFFFF0u);  // past the frame: no request
+    const uint32_t loads = (nb + P - 1) / P;  // <= S
+    auto issue = [&](uint32_t j) -> u32x4 {
+        uint32_t off = 0xFFFFFFF0u;  // past the block's loads, or the frame: no request
+        if (j < loads) {             // wave-uniform
+            const uint32_t g = j * P + gi;
+            const uint32_t Lg = (uint32_t)__shfl((int)Lc, (int)g, 64);
+            if (16u * k < Lg) off = g * stride + 16u * k;
         }
+        return buf_load<true>(rb, off);
+    };
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = issue(first + step * u);
+    for (uint32_t j0 = first; j0 < loads; j0 += step * U) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (t0 + u < loads) {  // wave-uniform
-                const uint32_t g = (t0 + u) * P + gi;
-                const int hi = (int)lg[u] - 16 * (int)k;
+            const uint32_t j = j0 + step * u;
+            if (j < loads) {  // wave-uniform
+                const uint32_t g = j * P + gi;
+                const int hi = (int)__shfl((int)Lc, (int)g, 64) - 16 * (int)k;
                 const u32x4 x = hi < 16 ? mask_tail(v[u], hi) : v[u];
                 const uint32_t tot = group_total<S>(dot4(x, 0u));
                 if (k == S / 2) t.sum[g] = tot;
                 if (k < 6) t.hdr[k][g] = x;
             }
+            v[u] = issue(j + step * U);
         }
     }
 }
 
-// Longer frames: item i of the wave's stream = row r of slot g, for the slots'
-// row counts R_g = ceil(chunks_g / 64) in slot order (incl = their inclusive
-// prefix, lane g).  Slot of item i: the number of slots whose rows all come
-// before it (a ballot popcount); its row: i minus the rows before the slot.
+// Longer frames: item i of the block's stream = row r of slot g, for the
+// slots' row counts R (lane g: R_g = ceil(chunks_g / 64); incl their inclusive
+// prefix).  Slot of item i: the number of slots whose rows all come before it
+// (a ballot popcount); its row: i minus the rows before the slot.  This wave
+// takes items first, first + step, ... below end; its run partial is flushed
+// (one wave reduce, an LDS add: slots may be shared between waves) when the
+// slot changes.
 template <int U>
-__device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride, uint32_t Lc, uint32_t R,
-                                          int lane) {
-    const uint32_t incl = wave_incl_scan(R);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // items
-    const uint32_t excl = incl - R;
+__device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride, uint32_t Lc, uint32_t incl,
+                                          uint32_t excl, uint32_t first, uint32_t end, uint32_t step, int lane) {
     u32x4 v[U];
     uint32_t sg[U], sr[U], sl[U];  // per ring entry: slot, row, slot bytes (scalars)
     auto issue = [&](uint32_t i, int u) {
         uint32_t g = 0, r = 0, L = 0;
-        if (i < T) {  // wave-uniform
+        if (i < end) {  // wave-uniform
             g = (uint32_t)__popcll(__ballot(incl <= i));
             r = i - (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)g);
             L = (uint32_t)__builtin_amdgcn_readlane((int)Lc, (int)g);
@@ -334,20 +348,21 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
         const uint32_t c = 64u * r + (uint32_t)lane;
         v[u] = buf_load<true>(rb, 16u * c < L ? g * stride + 16u * c : 0xFFFFFFF0u);
     };
+    auto flush = [&](uint32_t g, uint32_t acc) {
+        const uint32_t s = wave_total(acc);
+        if (lane == 0) atomicAdd(&t.sum[g], s);
+    };
 #pragma unroll
-    for (int u = 0; u < U; u++) issue((uint32_t)u, u);
+    for (int u = 0; u < U; u++) issue(first + step * u, u);
     uint32_t cur = 0xFFFFFFFFu, acc = 0;
-    for (uint32_t j0 = 0; j0 < T; j0 += U) {
+    for (uint32_t j0 = first; j0 < end; j0 += step * U) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = j0 + u;
-            if (i < T) {  // wave-uniform
+            const uint32_t i = j0 + step * u;
+            if (i < end) {  // wave-uniform
                 const uint32_t g = sg[u], r = sr[u];
-                if (g != cur) {  // the previous slot's rows are all in: one wave reduce
-                    if (cur != 0xFFFFFFFFu) {
-                        const uint32_t s = wave_total(acc);
-                        if (lane == 0) t.sum[cur] = s;
-                    }
+                if (g != cur) {  // this wave's share of the previous slot is all in
+                    if (cur != 0xFFFFFFFFu) flush(cur, acc);
                     cur = g;
                     acc = 0;
                 }
@@ -356,55 +371,76 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
                 acc = dot4(x, acc);
                 if (r == 0 && lane < 6) t.hdr[lane][g] = x;
             }
-            issue(i + U, u);  // past the stream: no request
+            issue(i + step * U, u);  // past this wave's items: no request
         }
     }
-    if (cur != 0xFFFFFFFFu) {
-        const uint32_t s = wave_total(acc);
-        if (lane == 0) t.sum[cur] = s;
-    }
+    if (cur != 0xFFFFFFFFu) flush(cur, acc);
 }
 
-template <int U>
+template <int U, int UD>
 __global__ __launch_bounds__(256) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
-                                              const uint16_t* __restrict__ lens, uint64_t n, uint32_t W,
-                                              uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
-    __shared__ RingLds s_ring[4];
+                                              const uint16_t* __restrict__ lens, uint64_t n, uint32_t G,
+                                              uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
+                                              uint32_t kflags) {
+    // (the block size is a compile-time constant: as a kernel argument it cost
+    // the short-frame stream 40 %, profiles/r05_ring_schedule_ab.jsonl)
+    constexpr uint32_t B = kRingB;
+    __shared__ RingLds t;
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    RingLds& t = s_ring[w];
-    const uint64_t p0 = ((uint64_t)blockIdx.x * 4u + w) * W;
-    if (p0 >= n) return;  // wave-uniform
-    const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)W, n - p0);
-    const bool valid = (uint32_t)lane < np;
-    const uint32_t L = valid ? (uint32_t)lens[p0 + lane] : 0u;
-    const bool bad = L > stride;              // longer than its slot: not read, verdict 0
-    const uint32_t Lc = bad ? 0u : L;         // the bytes this slot reads
+    const uint64_t b0 = (uint64_t)blockIdx.x * B;  // the block's first slot
+    const uint32_t nb = (uint32_t)min<uint64_t>(B, n - b0);
+    const bool valid = (uint32_t)lane < nb;
+    const uint32_t L = valid ? (uint32_t)lens[b0 + lane] : 0u;  // every wave: all 64 lengths
+    const bool bad = L > stride;       // longer than its slot: not read, verdict 0
+    const uint32_t Lc = bad ? 0u : L;  // the bytes this slot reads
     const uint32_t nch = (Lc + 15u) >> 4;
     const uint32_t cmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(nch), 63);
-    const buf_t rb = buf_rsrc(arena + p0 * stride, np * stride);  // the wave's slots
-    if (cmax <= 8)
-        ring_short<8, 8>(t, rb, stride, np, Lc, lane);
-    else if (cmax <= 16)
-        ring_short<16, 16>(t, rb, stride, np, Lc, lane);
-    else if (cmax <= 32)
-        ring_short<32, 16>(t, rb, stride, np, Lc, lane);
-    else
-        ring_rows<U>(t, rb, stride, Lc, (nch + 63u) >> 6, lane);
-    wave_sync();
+    if (w == 0) t.sum[lane] = 0;  // flushes add
+    __syncthreads();
+    const buf_t rb = buf_rsrc(arena + b0 * stride, nb * stride);  // the block's slots
+    if (cmax <= 32) {
+        if (cmax <= 8)
+            ring_short<8, 8>(t, rb, stride, nb, Lc, w, 4u, lane);
+        else if (cmax <= 16)
+            ring_short<16, 8>(t, rb, stride, nb, Lc, w, 4u, lane);
+        else
+            ring_short<32, 8>(t, rb, stride, nb, Lc, w, 4u, lane);
+    } else {
+        const uint32_t R = (nch + 63u) >> 6;
+        const uint32_t incl = wave_incl_scan(R);
+        const uint32_t excl = incl - R;
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // the block's items
+        const bool coop = (kflags & kRingAllCoop) || (!(kflags & kRingOwnSlots) && T >= kRingCoopRows * nb);
+        if (coop) {
+            // sub-groups of G slots, one after the other, the four waves on each
+            for (uint32_t g0 = 0; g0 < nb; g0 += G) {
+                const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)g0);
+                const uint32_t ie = g0 + G < nb ? (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)(g0 + G)) : T;
+                ring_rows<UD>(t, rb, stride, Lc, incl, excl, ib + w, ie, 4u, lane);
+            }
+        } else {  // wave w: the items of its quarter of the slots
+            const uint32_t q = B / 4u;
+            const uint32_t ib = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)(q * w));
+            const uint32_t ie = w < 3 ? (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)(q * w + q)) : T;
+            ring_rows<U>(t, rb, stride, Lc, incl, excl, ib, ie, 1u, lane);
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;  // wave 0 judges the block's slots
     uint32_t r = 0;
     if (valid && !bad) {
-        const uint32_t F = bswap16(fold16(nch ? t.sum[lane] : 0u));  // slots start 16-byte aligned: even address
+        const uint32_t F = bswap16(fold16(t.sum[lane]));  // slots start 16-byte aligned: even address
         uint32_t hw[24];
 #pragma unroll
         for (int k = 0; k < 6; k++) {  // chunks past the frame were never captured: zero
             const u32x4 x = 16u * k < L ? t.hdr[k][lane] : u32x4{0u, 0u, 0u, 0u};
             hw[4 * k] = x.x, hw[4 * k + 1] = x.y, hw[4 * k + 2] = x.z, hw[4 * k + 3] = x.w;
         }
-        r = rx_from_window(arena + (p0 + (uint32_t)lane) * stride, L, F, hw);
+        r = rx_from_window(arena + (b0 + (uint32_t)lane) * stride, L, F, hw);
     }
     if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
-    store_result8(buf_rsrc(ok + p0, np), (uint32_t)lane, r);
+    store_result8(buf_rsrc(ok + b0, nb), (uint32_t)lane, r);
 }
 
 int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
@@ -449,25 +485,36 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         PIPCK_LAUNCHED("k_ring_rx");
         return PIPCK_OK;
     }
-    // slot groups (k_ring).  W slots per wave: 64 up to 2 KiB slots, 32 up to 4
-    // KiB, 16 above, or tune bits 8..15 (16 / 32 / 64); U loads in flight in the
-    // row stream: 16, or loads_per_lane 8 / 24 / 32.
-    uint32_t W = stride <= 2048 ? 64u : (stride <= 4096 ? 32u : 16u);
-    const uint32_t wt = (flags >> 8) & 0xFFu;
-    if (wt == 16 || wt == 32 || wt == 64) W = wt;
-    const uint64_t blocks = (n + 4u * W - 1) / (4u * W);
+    // slot groups (k_ring): 64 slots per block; U = 8 loads in flight per wave in
+    // the row stream (loads_per_lane 16 / 24 for more): the kernel's registers --
+    // 48 VGPRs at 8, 79 at 16 -- set the waves per SIMD, which the short and
+    // sparse rings need more than a deeper ring (short 1 KiB slots 0.27 against
+    // 0.32 ms, sparse 9 KiB 1.32 against 1.46; full 1.5 KiB slots 0.846
+    // against 0.858 of peak: profiles/r05_ring_schedule_ab.jsonl)
+    const uint64_t blocks = (n + kRingB - 1) / kRingB;
+    // the interleaved row stream covers G slots at a time: 16 (jumbo slots 0.890
+    // against 0.879 of peak for all 64 at once), or the tune's blocks knob (8 / 32 / 64)
+    const uint32_t gt = g_tune_blocks();
+    const uint32_t G = (gt == 8 || gt == 32 || gt == 64) ? gt : 16u;
     if (blocks > 0x7FFFFFFFull) {
         set_error("pipck_rx_verify_ring: too many slots for one launch");
         return PIPCK_ERANGE;
     }
     const uint8_t* a = (const uint8_t*)d_arena;
     const uint32_t st = (uint32_t)stride;
+    // loads in flight per wave: U in the short and own-slot streams, UD in the
+    // interleaved one (loads_per_lane 16 / 24: both; 17 / 25: UD only)
+#define PIPCK_RING(UU, UUD)                                                                                     \
+    PIPCK_LAUNCH((k_ring<UU, UUD>), dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, G, d_ok, d_err,    \
+                 flags)
     switch (g_tune_loads()) {
-        case 8: PIPCK_LAUNCH(k_ring<8>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
-        case 24: PIPCK_LAUNCH(k_ring<24>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
-        case 32: PIPCK_LAUNCH(k_ring<32>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
-        default: PIPCK_LAUNCH(k_ring<16>, dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, W, d_ok, d_err); break;
+        case 16: PIPCK_RING(16, 16); break;
+        case 24: PIPCK_RING(24, 24); break;
+        case 17: PIPCK_RING(8, 16); break;
+        case 25: PIPCK_RING(8, 24); break;
+        default: PIPCK_RING(8, 8); break;
     }
+#undef PIPCK_RING
     PIPCK_LAUNCHED("k_ring");
     return PIPCK_OK;
 }

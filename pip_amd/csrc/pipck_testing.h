@@ -51,8 +51,9 @@ extern "C" {
  * kernels have them compiled out and ignore them otherwise.
  * Bit 28 = the other fixed-stride schedule (and for pipck_rx_verify_ring the
  * row stream k_ring_rx instead of the default k_ring; lanes_per_packet = 256
- * there selects k_ring_slots, and bits 8..15 = 16 / 32 / 64 set k_ring's slots
- * per wave, loads_per_lane 8 / 24 / 32 its loads in flight): k_flat (one task per wave)
+ * there selects k_ring_slots, loads_per_lane 8 / 24 k_ring's loads in flight,
+ * and bits 29 / 27 make k_ring's row stream never / always deal its items
+ * round-robin to the block's waves): k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
  * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
  * for k_flat_coop, bits 8..15 are rows per wave

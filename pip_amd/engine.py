@@ -482,12 +482,15 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          trace: bool = False, loads_only: bool = False, no_task_end: bool = False,
          end_no_store: bool = False, alt_flat_schedule: bool = False,
          plain_result_stores: bool = False, wave_stores: bool = False, free_run: bool = False,
-         packed_no_align: bool = False, hdr_in_place: bool = False) -> None:
+         packed_no_align: bool = False, hdr_in_place: bool = False, ring_own_slots: bool = False,
+         ring_all_coop: bool = False) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
     except the measurement-only probes loads_only (bit 21), no_task_end (22), end_no_store (23) and
     hdr_in_place (pipck_tune_probes bit 0, not a tune flag: k_hdr stores the results into the headers'
-    ip_sum and leaves the result array untouched).  alt_flat_schedule (bit 28) never changes results."""
+    ip_sum and leaves the result array untouched).  alt_flat_schedule (bit 28) never changes results.
+    ring_own_slots / ring_all_coop: k_ring's row stream never / always deals items round-robin to the
+    block's waves (bits 29 / 27, read by pipck_rx_verify_ring only)."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
@@ -496,7 +499,8 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
              | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0) | (1 << 22 if no_task_end else 0)
              | (1 << 23 if end_no_store else 0) | (1 << 28 if alt_flat_schedule else 0)
-             | (1 << 29 if plain_result_stores else 0) | (1 << 30 if (wave_stores or packed_no_align) else 0)
+             | (1 << 29 if (plain_result_stores or ring_own_slots) else 0) | (1 << 27 if ring_all_coop else 0)
+             | (1 << 30 if (wave_stores or packed_no_align) else 0)
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
     load().pipck_tune_probes(1 if hdr_in_place else 0)

@@ -86,7 +86,10 @@ def test_product_sources_read_no_environment():
 
 def test_libpipck_loads_and_reports_version():
     lib = _lib.load()
-    assert lib.pipck_version() >> 16 == 1
+    text = (ROOT / "include" / "pipck.h").read_text()
+    major = int(re.search(r"#define PIPCK_VERSION_MAJOR (\d+)", text).group(1))
+    minor = int(re.search(r"#define PIPCK_VERSION_MINOR (\d+)", text).group(1))
+    assert lib.pipck_version() == (major << 16 | minor) and major == 1 and minor >= 2
     assert lib.pipck_cfg_seed(5) == 0x9E3779B97F4A7C15 ^ 5
 
 
@@ -101,7 +104,12 @@ def test_shim_exports_pip_mangled_names():
     syms = dynsyms(_lib.LIBSHIM)
     assert set(PIP_MANGLED) <= syms
     # the RX batch verifier is extern "C" (include/pip_checksum_amd.h)
-    assert "pip_checksum_amd_verify_packets" in syms
+    assert "pip_checksum_amd_verify_packets" in syms and "pip_checksum_amd_rx_abi" in syms
+    # the RX verdict meaning (7 = verified) is versioned, in the header and in the library
+    shim = C.CDLL(str(_lib.LIBSHIM))
+    shim.pip_checksum_amd_rx_abi.restype = C.c_uint32
+    assert shim.pip_checksum_amd_rx_abi() == 2
+    assert "#define PIP_CHECKSUM_AMD_RX_ABI 2" in (ROOT / "include" / "pip_checksum_amd.h").read_text()
     needed = subprocess.run(["readelf", "-d", str(_lib.LIBSHIM)], check=True, capture_output=True, text=True).stdout
     assert "libpipck.so" in needed
 

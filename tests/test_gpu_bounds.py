@@ -119,7 +119,7 @@ def _ipv4_frame(oracle, rng, l4len, k, total_override=None):
     return bytes(p)
 
 
-@pytest.mark.parametrize("schedule", ["groups", "rows", "slots"])
+@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots"])
 @pytest.mark.parametrize("stride", [1024, 9216])
 def test_ring_length_past_the_slot_is_an_error_not_a_fault(oracle, schedule, stride):
     """pipck_rx_verify_ring_n through ctypes, no Python guard, on a ring hipMalloc'd
@@ -172,9 +172,9 @@ def test_ring_length_past_the_slot_is_an_error_not_a_fault(oracle, schedule, str
         # the untampered lengths: nothing refused, the middle slot judged again
         lens_ok = np.array([len(f) for f in frames], dtype=np.uint16)
         err.zero_()
-        rc = lib.pipck_rx_verify_ring_n(ring.ptr, C.c_uint64(stride),
-                                        _p(torch.from_numpy(lens_ok.view(np.int16)).to("cuda")), C.c_uint64(n), _p(ok),
-                                        _p(err), C.c_void_p(0))
+        dl_ok = torch.from_numpy(lens_ok.view(np.int16)).to("cuda")  # held across the call
+        rc = lib.pipck_rx_verify_ring_n(ring.ptr, C.c_uint64(stride), _p(dl_ok), C.c_uint64(n), _p(ok), _p(err),
+                                        C.c_void_p(0))
         assert rc == 0
         torch.cuda.synchronize()
         assert int(err.item()) == 0 and np.array_equal(ok.cpu().numpy(), host)
@@ -196,13 +196,13 @@ def _ragged_case(n_flows=8):
 
 def _tamper(offs, lens, flows, size, n_flows):
     offs, lens, flows = offs.copy(), lens.copy(), flows.copy()
-    bad = {3: "far", 70: "straddles", 71: "overflow", 150: "flow", 200: "ends_exactly", 330: "len0_past"}
+    bad = {3: "far", 70: "straddles", 71: "overflow", 150: "flow", 200: "ends_exactly", 328: "len0_past"}
     offs[3] = size * 100
     offs[70], lens[70] = size - 10, 20
     offs[71], lens[71] = (1 << 64) - 8, 64
     flows[150] = n_flows + 3
     offs[200], lens[200] = size - 64, 64  # ends exactly at the arena's end: allowed
-    offs[330], lens[330] = size + 1, 0     # empty, but past the end
+    offs[328], lens[328] = size + 1, 0     # empty, but past the end (the last descriptor)
     refused = [i for i, why in bad.items() if why != "ends_exactly"]
     return offs, lens, flows, refused
 
@@ -289,10 +289,10 @@ def test_chains_bounded_by_arena_segments_and_flows(oracle):
     out = torch.zeros(n_pk, dtype=torch.int16, device="cuda")
     err = torch.zeros(1, dtype=torch.int32, device="cuda")
     lib = _lib.load()
-    rc = lib.pipck_checksum_chains_n(_p(arena), C.c_uint64(host.size), _p(segs), C.c_uint64(n_segs),
-                                     _p(torch.from_numpy(sb_bad).to("cuda")),
-                                     _p(torch.from_numpy(pkt_flow).to("cuda")), C.c_uint64(n_pk), _p(pseudo),
-                                     C.c_uint32(n_flows), _p(scratch), _p(out), _p(err), C.c_void_p(0))
+    d_sb, d_flow = torch.from_numpy(sb_bad).to("cuda"), torch.from_numpy(pkt_flow).to("cuda")  # held across the call
+    rc = lib.pipck_checksum_chains_n(_p(arena), C.c_uint64(host.size), _p(segs), C.c_uint64(n_segs), _p(d_sb),
+                                     _p(d_flow), C.c_uint64(n_pk), _p(pseudo), C.c_uint32(n_flows), _p(scratch),
+                                     _p(out), _p(err), C.c_void_p(0))
     torch.cuda.synchronize()
     assert rc == 0, lib.pipck_last_error()
     got = out.cpu().numpy().view(np.uint16)

@@ -417,7 +417,8 @@ def _ring(frames, stride):
 # pipck_rx_verify_ring's three schedules (pipck_rxdev.hip): the default slot
 # groups (k_ring), the row stream (k_ring_rx, tune flag bit 28) and slot by slot
 # (k_ring_slots, the wave-per-packet arm)
-RING_KERNELS = {"groups": "k_ring<", "rows": "k_ring_rx", "slots": "k_ring_slots"}
+RING_KERNELS = {"groups": "k_ring<8, 8>", "own": "k_ring<8, 8>", "coop": "k_ring<8, 8>", "rows": "k_ring_rx",
+                "slots": "k_ring_slots"}
 
 
 def _ring_schedule(name):
@@ -427,6 +428,10 @@ def _ring_schedule(name):
         engine.tune(alt_flat_schedule=True)
     elif name == "slots":
         engine.tune(lanes_per_packet=256)
+    elif name == "own":  # k_ring's row stream: each wave its own 16 slots
+        engine.tune(ring_own_slots=True)
+    elif name == "coop":  # k_ring's row stream: items dealt round-robin to the block's waves
+        engine.tune(ring_all_coop=True)
     else:
         engine.tune()
 
@@ -462,7 +467,7 @@ def _host_bits(frames):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fill", ["mixed", "short"])
-@pytest.mark.parametrize("schedule", ["groups", "rows", "slots"])
+@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots"])
 @pytest.mark.parametrize("stride", [1024, 2048, 9216])
 def test_rx_verify_ring_equals_host_path(oracle, stride, schedule, fill):
     """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
@@ -542,7 +547,7 @@ def test_rx_verify_ring_dense_and_short_full_size(stride, l4_len):
             assert RING_KERNELS[schedule] in _last_kernel()
         finally:
             engine.tune()
-    assert torch.equal(got["groups"], got["rows"]) and torch.equal(got["groups"], got["slots"])
+    assert all(torch.equal(got["groups"], got[k]) for k in got)
     ok = got["groups"]
     n_ok = int((ok == VERIFIED).sum().item())
     assert n_ok > n - 1000 and int((ok == UNCHECKED).sum().item()) == n - n_ok
@@ -567,8 +572,8 @@ def test_rx_verify_ring_default_schedule(oracle, stride):
         frames.append(bytes(p))
     ring, lens = _ring(frames, stride)
     dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
-    assert "k_ring<" in _last_kernel()
-    for schedule in ("rows", "slots"):
+    assert RING_KERNELS["groups"] in _last_kernel()
+    for schedule in ("own", "coop", "rows", "slots"):
         _ring_schedule(schedule)
         try:
             other = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()

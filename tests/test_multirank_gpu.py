@@ -265,3 +265,49 @@ def test_bench_line_names_its_kernel_and_build():
     # 100000 packets is not the profiled batch: no traffic may be attached
     assert rf["traffic"] is None and "mismatch" in rf["traffic_source"]
     assert d["per_rank_device"][0]["pci_bus_id"]
+
+
+@pytest.mark.parametrize("launcher", ["self", "torchrun"])
+def test_bench_eight_ranks_rehearsal(launcher):
+    """the driver's 8-GPU SCALE line, rehearsed on this box.
+    `bench.py --gpus 8` self-launched and under torch.distributed.run
+    --nproc-per-node 8, 1M cfg5 packets per rank: one JSON line with 8
+    per_rank_device records, the distinct GPUs it really ran on (SHARING when the
+    box has fewer than 8), and each rank's results digest -- rank 5's shard
+    (packet ids 5M .. 6M) equals a one-rank run of the same ids here."""
+    import hashlib
+
+    import torch
+
+    from pip_amd import engine
+    from pip_amd.workloads import CFG5, N_FLOWS
+
+    per = 1 << 20
+    args = [str(ROOT / "bench.py"), "--gpus", "8", "--steps", "3", "--warmup", "1", "--packets-per-gpu", str(per),
+            "--no-cpu", "--digest", *share_flag(8)]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), *args]
+    else:
+        cmd = [sys.executable, *args]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["scaling"] == "weak"
+    assert d["config"]["global_packets"] == 8 * per and d["per_rank_packets"] == [per] * 8
+    assert [p["rank"] for p in d["per_rank_device"]] == list(range(8))
+    assert d["distinct_gpus"] == min(8, n_visible())
+    if n_visible() < 8:
+        assert f"8 ranks SHARING {n_visible()} GPU(s)" in d["config"]["parallelism"]
+    recs = d["per_rank_results"]
+    assert [(x["rank"], x["first"], x["count"]) for x in recs] == [(k, k * per, per) for k in range(8)]
+    # a one-rank run of rank 5's packet ids, in this process
+    w, first = CFG5, recs[5]["first"]
+    arena = torch.empty(per * w.stride, dtype=torch.uint8, device="cuda")
+    engine.gen_fixed(arena, w.stride, w.length, per, first, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(w.family, N_FLOWS, w.seed, w.proto)
+    one = engine.checksum_fixed(arena, w.stride, w.length, per, pseudo, N_FLOWS, None, first)
+    assert hashlib.sha256(one.cpu().numpy().tobytes()).hexdigest() == recs[5]["sha256"]
+    assert len({x["sha256"] for x in recs}) == 8  # every shard its own packets

@@ -55,8 +55,12 @@ def main():
     ap.add_argument("--rings", default="ring_sparse_9216,ring_dense_1536,ring_dense_9216,ring_short_2048,ring_short_1024")
     ap.add_argument("--tune", default="{}", help="engine.tune kwargs for the default (groups) arm, JSON")
     ap.add_argument("--skip-packed", action="store_true", help="rings only")
+    ap.add_argument("--arms", default="groups,rows,slots",
+                    help="ring schedules to time; groups:NAME = the default with --tunes[NAME]")
+    ap.add_argument("--tunes", default="{}", help='JSON {"NAME": engine.tune kwargs} for groups:NAME arms')
     a = ap.parse_args()
     tune_default = json.loads(a.tune)
+    tunes = json.loads(a.tunes)
     import torch
 
     from bench import last_kernel
@@ -97,7 +101,10 @@ def main():
     # L4 in 9,216-B slots) and short frames in small slots (200-B L4 in 2 KiB,
     # 100-B L4 in 1 KiB)
     rings = (("ring_sparse_9216", 9216, 0, n), ("ring_dense_1536", 1536, 1480, n), ("ring_dense_9216", 9216, 8900, n // 2),
-             ("ring_short_2048", 2048, 200, n), ("ring_short_1024", 1024, 100, n))
+             ("ring_short_2048", 2048, 200, n), ("ring_short_1024", 1024, 100, n),
+             # probes (not in the default set): every slot filled to the byte (IPv4 frames of 9,216 B;
+             # IPv6 ones 20 B longer would not fit, so the L4 length leaves room for both)
+             ("ring_full_9216", 9216, 9216 - 40, n // 2), ("ring_full_1536", 1536, 1536 - 40, n))
     for tag, stride, l4_len, m in [r for r in rings if r[0] in a.rings.split(",")]:
         del arena
         torch.cuda.empty_cache()
@@ -112,7 +119,7 @@ def main():
         # the three schedules, rounds interleaved, verdicts equal: the default slot
         # groups (k_ring), the row stream (k_ring_rx, flag bit 28) and slot by slot
         # (k_ring_slots, the wave-per-packet arm)
-        ts = {"groups": [], "rows": [], "slots": []}
+        ts = {k: [] for k in a.arms.split(",")}
         got = {}
         for _ in range(a.rounds):
             for arm in ts:
@@ -120,6 +127,8 @@ def main():
                     engine.tune(lanes_per_packet=256)
                 elif arm == "rows":
                     engine.tune(alt_flat_schedule=True)
+                elif arm.startswith("groups:"):
+                    engine.tune(**tunes[arm.split(":", 1)[1]])
                 else:
                     engine.tune(**tune_default)
                 for _ in range(a.warm):
@@ -127,7 +136,8 @@ def main():
                 ts[arm].append(timed_b2b(rfn, a.iters))
                 got[arm] = (last_kernel().split("(")[0], rok.clone())
         engine.tune()
-        assert torch.equal(got["rows"][1], got["slots"][1]) and torch.equal(got["groups"][1], got["slots"][1])
+        arms = list(got)
+        assert all(torch.equal(got[arms[0]][1], got[k][1]) for k in arms)
         for arm, tl in ts.items():
             mr = statistics.median(tl)
             h = {int(k): int(c) for k, c in zip(*__import__("numpy").unique(got[arm][1].cpu().numpy(), return_counts=True))}
