@@ -447,8 +447,12 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
     flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto) if w.family else b""
     gpu = gpu_out.cpu().numpy().view(np.uint16)
 
+    # the sample BASELINE.md ("Which inputs") prescribes: the full batch for cfg1-cfg4,
+    # the first 1M packets for cfg5 (64M x 8,980 B cannot be host-resident) -- up to
+    # ~9 GB of host memory (cfg3, cfg5); --cpu-sample overrides it
+    plan = f"BASELINE.md plan: {'first 1M packets of the per-GPU shard' if w.cfg == 5 else 'the full batch'}"
     if w.ragged:
-        n = args.cpu_sample or min(count, 1 << 21)  # ~2M Zipf packets, ~2 GB
+        n = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)
         arena, offs, lens = orc.gen_ragged_batch(w.seed, first, n, w.hdr, threads)
         l4 = int(lens.astype(np.int64).sum())
 
@@ -464,7 +468,8 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
         run(1)
         st = l4 / (time.perf_counter() - t0) / 2**30
         cpu = {"value": round(l4 * reps / el / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-               "sample": f"first {n} packets of the same Zipf workload ({l4 / 2**30:.2f} GiB of L4 bytes), "
+               "sample": f"first {n} packets of the same Zipf workload ({l4 / 2**30:.2f} GiB of L4 bytes; "
+                         f"{plan if not args.cpu_sample else '--cpu-sample'}), "
                          f"pip_inet_checksum per packet, {reps} timed passes on {threads} threads; "
                          f"1 thread: {st:.3f} GiB/s",
                "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified,
@@ -473,8 +478,7 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
             {"value": None, "note": "host end-to-end: rank 0 of a one-rank run only"}
         return cpu, e2e
 
-    # fixed strides: cfg1's whole 1M-header batch is a 20 MB sample; others ~2 GiB
-    n = args.cpu_sample or min(count, max(1, (2 << 30) // w.stride))
+    n = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)
     lib = _lib.load()
     pin = lib.pipck_host_alloc(n * w.stride)
     if not pin:
@@ -516,7 +520,8 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
         lib.pipck_host_free(pin)
     what = "pip_ip_checksum" if not w.family else f"pip_inet{'6' if w.family == 6 else ''}_checksum"
     cpu = {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-           "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.3f} GiB), {what} per packet, "
+           "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.3f} GiB; "
+                     f"{plan if not args.cpu_sample else '--cpu-sample'}), {what} per packet, "
                      f"{reps} timed passes on {threads} threads; 1 thread: {st:.3f} GiB/s",
            "single_core_gib_per_s": round(st, 3),
            "mpkt_per_s": round(n * reps / el / 1e6, 2), "single_core_mpkt_per_s": round(n * reps1 / el1 / 1e6, 2),

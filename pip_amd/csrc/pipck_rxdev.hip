@@ -336,7 +336,10 @@ template <int U>
 __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride, uint32_t Lc, uint32_t incl,
                                           uint32_t excl, uint32_t first, uint32_t end, uint32_t step, int lane) {
     u32x4 v[U];
-    uint32_t sg[U], sr[U], sl[U];  // per ring entry: slot, row, slot bytes (scalars)
+    // per ring entry, one scalar: slot g (6 bits) | row r << 6 (6 bits: <= 64 rows
+    // in a 64 KiB slot) | slot bytes L << 12 (17 bits) -- three scalars per entry
+    // would take the kernel past 80 SGPRs, which costs a block per CU
+    uint32_t se[U];
     auto issue = [&](uint32_t i, int u) {
         uint32_t g = 0, r = 0, L = 0;
         if (i < end) {  // wave-uniform
@@ -344,7 +347,7 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
             r = i - (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)g);
             L = (uint32_t)__builtin_amdgcn_readlane((int)Lc, (int)g);
         }
-        sg[u] = g, sr[u] = r, sl[u] = L;
+        se[u] = g | r << 6 | L << 12;
         const uint32_t c = 64u * r + (uint32_t)lane;
         v[u] = buf_load<true>(rb, 16u * c < L ? g * stride + 16u * c : 0xFFFFFFF0u);
     };
@@ -360,14 +363,17 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
         for (int u = 0; u < U; u++) {
             const uint32_t i = j0 + step * u;
             if (i < end) {  // wave-uniform
-                const uint32_t g = sg[u], r = sr[u];
+                const uint32_t g = se[u] & 63u, r = (se[u] >> 6) & 63u, L = se[u] >> 12;
                 if (g != cur) {  // this wave's share of the previous slot is all in
                     if (cur != 0xFFFFFFFFu) flush(cur, acc);
                     cur = g;
                     acc = 0;
                 }
-                const int hi = (int)sl[u] - 16 * (int)(64u * r + (uint32_t)lane);
-                const u32x4 x = hi < 16 ? mask_tail(v[u], hi) : v[u];
+                u32x4 x = v[u];
+                if (L < 1024u * (r + 1u)) {  // wave-uniform: the frame ends in this row (else no mask)
+                    const int hi = (int)L - 16 * (int)(64u * r + (uint32_t)lane);
+                    if (hi < 16) x = mask_tail(x, hi);
+                }
                 acc = dot4(x, acc);
                 if (r == 0 && lane < 6) t.hdr[lane][g] = x;
             }
@@ -378,7 +384,7 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
 }
 
 template <int U, int UD>
-__global__ __launch_bounds__(256) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
                                               const uint16_t* __restrict__ lens, uint64_t n, uint32_t G,
                                               uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
                                               uint32_t kflags) {
@@ -508,11 +514,12 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     PIPCK_LAUNCH((k_ring<UU, UUD>), dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, G, d_ok, d_err,    \
                  flags)
     switch (g_tune_loads()) {
+        case 8: PIPCK_RING(8, 8); break;
         case 16: PIPCK_RING(16, 16); break;
         case 24: PIPCK_RING(24, 24); break;
-        case 17: PIPCK_RING(8, 16); break;
-        case 25: PIPCK_RING(8, 24); break;
-        default: PIPCK_RING(8, 8); break;
+        case 17: PIPCK_RING(12, 16); break;
+        case 25: PIPCK_RING(12, 24); break;
+        default: PIPCK_RING(12, 12); break;
     }
 #undef PIPCK_RING
     PIPCK_LAUNCHED("k_ring");

@@ -247,7 +247,7 @@ static void run(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out, ui
 #define PROBE_CASE(u, w) \
     if (m.U == u && m.WPB == w) return launch<u, w>(m, a, rows, out, ctr, cus);
     PROBE_CASE(16, 4) PROBE_CASE(24, 4) PROBE_CASE(32, 4) PROBE_CASE(24, 1) PROBE_CASE(24, 2) PROBE_CASE(24, 8)
-    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8)
+    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8) PROBE_CASE(32, 1)
     fprintf(stderr, "no instance U=%d WPB=%d\n", m.U, m.WPB);
     exit(2);
 }
@@ -271,6 +271,8 @@ int main(int argc, char** argv) {
         {"pol_plain", 32, 4, 64, 40}, {"pol_nt", 32, 4, 64, 41}, {"pol_sc0", 32, 4, 64, 42},
         {"pol_sc0_nt", 32, 4, 64, 43}, {"pol_sc1", 32, 4, 64, 44}, {"pol_sc1_nt", 32, 4, 64, 45},
         {"pol_sc0_sc1", 32, 4, 64, 46}, {"pol_sc0_sc1_nt", 32, 4, 64, 47},
+        // k_packedb's schedule (cfg4): one ~64-row tile per one-wave block, a ring of 32 rows
+        {"disp_u32_w1_t64", 32, 1, 64, 0}, {"disp_u32_w1_t128", 32, 1, 128, 0}, {"disp_u24_w1_t64", 24, 1, 64, 0},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";

@@ -105,7 +105,7 @@ def main():
              # probes (not in the default set): every slot filled to the byte (IPv4 frames of 9,216 B;
              # IPv6 ones 20 B longer would not fit, so the L4 length leaves room for both)
              ("ring_full_9216", 9216, 9216 - 40, n // 2), ("ring_full_1536", 1536, 1536 - 40, n))
-    for tag, stride, l4_len, m in [r for r in rings if r[0] in a.rings.split(",")]:
+    for tag, stride, l4_len, m in [r for r in rings if r[0] in a.rings.split(",")]:  # --rings none: packed only
         del arena
         torch.cuda.empty_cache()
         ring, rlens, _ = engine.gen_rx_ring(m, 11, stride, l4_len=l4_len)
