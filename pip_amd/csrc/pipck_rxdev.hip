@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ 
 // the block's barrier wave 0 judges the 64 slots (lane g: slot g) with
 // rx_from_window, so one wave's parse is spread over 64 slots.
 constexpr uint32_t kRingB = 64;               // slots per block
-constexpr uint32_t kRingCoopRows = 4;         // mean rows per slot from which the waves interleave
+constexpr uint32_t kRingCoopRows = 2;         // mean rows per slot from which the waves interleave
 constexpr uint32_t kRingOwnSlots = 1u << 29;  // pipck_tune flag (ring only): never interleave
 constexpr uint32_t kRingAllCoop = 1u << 27;   // pipck_tune flag (ring only): always interleave
 
@@ -498,10 +498,12 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     // 0.32 ms, sparse 9 KiB 1.32 against 1.46; full 1.5 KiB slots 0.846
     // against 0.858 of peak: profiles/r05_ring_schedule_ab.jsonl)
     const uint64_t blocks = (n + kRingB - 1) / kRingB;
-    // the interleaved row stream covers G slots at a time: 16 (jumbo slots 0.890
-    // against 0.879 of peak for all 64 at once), or the tune's blocks knob (8 / 32 / 64)
+    // the interleaved row stream covers all 64 slots at once, or G at a time (the
+    // tune's blocks knob, 8 / 16 / 32): sub-groups helped jumbo slots only with a
+    // ring of 24 (0.890 against 0.879 of peak) and drain a shallow ring between
+    // groups of short slots (full 1.5 KiB slots 2.46 against 1.86 ms)
     const uint32_t gt = g_tune_blocks();
-    const uint32_t G = (gt == 8 || gt == 32 || gt == 64) ? gt : 16u;
+    const uint32_t G = (gt == 8 || gt == 16 || gt == 32) ? gt : 64u;
     if (blocks > 0x7FFFFFFFull) {
         set_error("pipck_rx_verify_ring: too many slots for one launch");
         return PIPCK_ERANGE;
@@ -515,11 +517,12 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
                  flags)
     switch (g_tune_loads()) {
         case 8: PIPCK_RING(8, 8); break;
+        case 12: PIPCK_RING(12, 12); break;
         case 16: PIPCK_RING(16, 16); break;
         case 24: PIPCK_RING(24, 24); break;
-        case 17: PIPCK_RING(12, 16); break;
-        case 25: PIPCK_RING(12, 24); break;
-        default: PIPCK_RING(12, 12); break;
+        case 17: PIPCK_RING(8, 16); break;
+        case 25: PIPCK_RING(8, 24); break;
+        default: PIPCK_RING(8, 12); break;
     }
 #undef PIPCK_RING
     PIPCK_LAUNCHED("k_ring");

@@ -417,7 +417,7 @@ def _ring(frames, stride):
 # pipck_rx_verify_ring's three schedules (pipck_rxdev.hip): the default slot
 # groups (k_ring), the row stream (k_ring_rx, tune flag bit 28) and slot by slot
 # (k_ring_slots, the wave-per-packet arm)
-RING_KERNELS = {"groups": "k_ring<12, 12>", "own": "k_ring<12, 12>", "coop": "k_ring<12, 12>", "rows": "k_ring_rx",
+RING_KERNELS = {"groups": "k_ring<8, 12>", "own": "k_ring<8, 12>", "coop": "k_ring<8, 12>", "rows": "k_ring_rx",
                 "slots": "k_ring_slots"}
 
 

@@ -28,6 +28,9 @@ for s in ${STEPS:-ring}; do
              || { echo "probe rc=$?"; exit 1; }
            timeout -k 10 300 python3 bench.py --workload cfg4 --no-cpu > "$OUT/bench_cfg4_${TAG}.json" \
              2> "$OUT/bench_cfg4_${TAG}.err" || { echo "bench rc=$?"; exit 1; } ;;
+    pytest) timeout -k 10 1200 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+             > "$OUT/pytest_${TAG}.log" 2>&1 || { echo "pytest failed"; tail -30 "$OUT/pytest_${TAG}.log"; exit 1; }
+           tail -1 "$OUT/pytest_${TAG}.log" ;;
     pmcrx) TAG=$TAG bash tools/pmc_rx.sh > "$OUT/pmc_rx_${TAG}.log" 2>&1 || { echo "pmcrx failed"; exit 1; } ;;
     *) echo "unknown step $s" ;;
   esac
