@@ -146,8 +146,10 @@ int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint6
  * boundary at or above it).  A tile of 64 packets whose chunks, as d_tile_chunk
  * and d_lens place them, reach past the arena -- a stale or foreign index --
  * is not read at all: each of its packets gets 0 (d_ok 0) and d_err (optional,
- * device u32) is OR-ed with (1 << PIPCK_ERANGE).  The plain names above trust
- * the index (arena_bytes unbounded). */
+ * device u32) is OR-ed with (1 << PIPCK_ERANGE).  With d_flow_of and n_flows >
+ * 0, an entry >= n_flows gives its packet 0 and sets the same bit (n_flows 0:
+ * the entries are trusted).  The plain names above trust the index and the
+ * flow entries (arena_bytes unbounded). */
 int pipck_checksum_packed_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                             const uint64_t* d_tile_chunk, uint64_t n_packets, const uint32_t* d_pseudo,
                             uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
@@ -179,7 +181,8 @@ int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const
                               const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok, void* stream);
 /* Bounded forms, as pipck_checksum_packed_n: a tile whose bytes reach past
  * arena_bytes (readable to the 16-byte boundary at or above it) is not read;
- * its packets get 0 and d_err gets (1 << PIPCK_ERANGE). */
+ * its packets get 0 and d_err gets (1 << PIPCK_ERANGE); d_flow_of entries are
+ * bounded by n_flows as there. */
 int pipck_checksum_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                                   const uint64_t* d_tile_off, uint64_t n_packets, const uint32_t* d_pseudo,
                                   uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,

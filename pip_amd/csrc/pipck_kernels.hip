@@ -1324,9 +1324,12 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
     const bool valid = seg < n;
     const uint32_t len = valid ? lens[seg] : 0u;
     uint32_t Pbase = 0;
+    bool fbad = false;  // a flow_of entry past the table (n_flows bounds it in the _n forms): result 0
     if (pseudo && valid) {  // loaded now so the tile's end waits on nothing
         const uint32_t f0 = (uint32_t)((flow_origin + tile * 64) % n_flows);  // one 64-bit modulo per tile
-        Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
+        const uint32_t f = flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows;
+        fbad = f >= n_flows;
+        Pbase = fbad ? 0u : pseudo[f];
     }
     // The tile's row grid starts on the 128-B line holding its first byte: the
     // `lead` chunks before it (the previous tile's last bytes) are loaded and
@@ -1359,7 +1362,11 @@ __global__ __launch_bounds__(64) void k_packed(const uint8_t* __restrict__ arena
                                                          true, MARKS ? kflags | kPackedMarksOnly : kflags, lead);
     const uint32_t F = bswap16(fold16(le_sum));  // 16-byte aligned: even address
     const uint32_t P = pseudo ? Pbase + len : 0u;
-    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    if (fbad) {
+        r = 0;
+        if (err) atomicOr(err, 1u << PIPCK_ERANGE);
+    }
     if (kflags & kPlainResultStores) {
         if (valid) {
             if (VERIFY)
@@ -1868,10 +1875,11 @@ static void launch_packed_u(bool nt, uint64_t tiles, hipStream_t s, const uint8_
                            fo, origin, out, ok, f, ach, err);
 }
 
+// bounded: the _n forms (flow_of entries bounded by n_flows when it is given)
 static int launch_packed(bool verify, const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                          const uint64_t* d_tile_chunk, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
                          const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok,
-                         uint32_t* d_err, hipStream_t s) {
+                         uint32_t* d_err, hipStream_t s, bool bounded = true) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_lens || !d_tile_chunk || (verify ? !d_ok : !d_out)) {
         set_error("pipck_checksum_packed: null pointer");
@@ -1900,7 +1908,8 @@ static int launch_packed(bool verify, const void* d_arena, uint64_t arena_bytes,
     const uint32_t f = g_tune.flags.load() ^ kPackedMarksOnly;
     const bool nt = nt_for(true);
     const uint8_t* a = (const uint8_t*)d_arena;
-    const uint32_t nf = n_flows ? n_flows : 1u;
+    // the kernel's n_flows: the modulus without flow_of; with it, the bound of its entries
+    const uint32_t nf = d_flow_of ? (bounded && n_flows ? n_flows : UINT32_MAX) : (n_flows ? n_flows : 1u);
     // rows in flight per wave: 17/25/33 = rings of 16/24/32
     switch (g_tune.loads.load()) {
         case 17: verify ? launch_packed_u<true, 16>(nt, tiles, s, a, d_lens, d_tile_chunk, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, f, ach, d_err)
@@ -2105,15 +2114,15 @@ int pipck_verify_packed_n(const void* d_arena, uint64_t arena_bytes, const uint1
 int pipck_checksum_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
                           const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
                           uint16_t* d_out, void* stream) {
-    return pipck_checksum_packed_n(d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
-                                   flow_origin, d_out, nullptr, stream);
+    return launch_packed(false, d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                         flow_origin, d_out, nullptr, nullptr, as_stream(stream), false);
 }
 
 int pipck_verify_packed(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_chunk, uint64_t n,
                         const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
                         uint8_t* d_ok, void* stream) {
-    return pipck_verify_packed_n(d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
-                                 flow_origin, d_ok, nullptr, stream);
+    return launch_packed(true, d_arena, UINT64_MAX, d_lens, d_tile_chunk, n, d_pseudo, n_flows, d_flow_of,
+                         flow_origin, nullptr, d_ok, nullptr, as_stream(stream), false);
 }
 
 int pipck_packed_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_chunk, void* stream) {

@@ -200,9 +200,12 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const ui
     const bool valid = seg < n;
     const uint32_t len = valid ? lens[seg] : 0u;
     uint32_t Pbase = 0;
+    bool fbad = false;  // a flow_of entry past the table (n_flows bounds it in the _n forms): result 0
     if (pseudo && valid) {  // loaded now so the tile's end waits on nothing
         const uint32_t f0 = (uint32_t)((flow_origin + tile * 64) % n_flows);
-        Pbase = pseudo[flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows];
+        const uint32_t f = flow_of ? flow_of[seg] : (f0 + (uint32_t)lane) % n_flows;
+        fbad = f >= n_flows;
+        Pbase = fbad ? 0u : pseudo[f];
     }
     const uint32_t nv = (uint32_t)min<uint64_t>(64, n - tile * 64);
     const uint32_t incl = wave_incl_scan(len);
@@ -263,8 +266,13 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const ui
             }
         }
         r = valid ? rx_from_window(pk, len, F, hw) : 0u;
-    } else
+    } else {
         r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+        if (fbad) {
+            r = 0;
+            if (err) atomicOr(err, 1u << PIPCK_ERANGE);
+        }
+    }
     if (VERIFY)  // write-through result stores (store_result16); lanes past the batch are range-checked off
         store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, r);
     else
@@ -328,10 +336,11 @@ __global__ __launch_bounds__(1024) void k_packedb_tile_scan(uint64_t* __restrict
     if (i == 0) tile_off[0] = 0;
 }
 
+// bounded: the _n forms (flow_of entries bounded by n_flows when it is given)
 static int launch_packedb(bool verify, const void* d_arena, uint64_t arena_bytes, const uint16_t* d_lens,
                           const uint64_t* d_tile_off, uint64_t n, const uint32_t* d_pseudo, uint32_t n_flows,
                           const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out, uint8_t* d_ok,
-                          uint32_t* d_err, hipStream_t s) {
+                          uint32_t* d_err, hipStream_t s, bool bounded = true) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || !d_lens || !d_tile_off || (verify ? !d_ok : !d_out)) {
         set_error("pipck_checksum_packed_bytes: null pointer");
@@ -350,7 +359,8 @@ static int launch_packedb(bool verify, const void* d_arena, uint64_t arena_bytes
         set_error("pipck_checksum_packed_bytes: more than 2^37 packets in one launch");
         return PIPCK_ERANGE;
     }
-    const uint32_t nf = n_flows ? n_flows : 1u;
+    // the kernel's n_flows: the modulus without flow_of; with it, the bound of its entries
+    const uint32_t nf = d_flow_of ? (bounded && n_flows ? n_flows : UINT32_MAX) : (n_flows ? n_flows : 1u);
     // a ring of 32 rows, non-temporal loads, as k_packed
     if (verify)
         PIPCK_LAUNCH((k_packedb<true, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
@@ -414,15 +424,15 @@ int pipck_verify_packed_bytes_n(const void* d_arena, uint64_t arena_bytes, const
 int pipck_checksum_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
                                 const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                                 uint64_t flow_origin, uint16_t* d_out, void* stream) {
-    return pipck_checksum_packed_bytes_n(d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
-                                         flow_origin, d_out, nullptr, stream);
+    return launch_packedb(false, d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                          flow_origin, d_out, nullptr, nullptr, as_stream(stream), false);
 }
 
 int pipck_verify_packed_bytes(const void* d_arena, const uint16_t* d_lens, const uint64_t* d_tile_off, uint64_t n,
                               const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                               uint64_t flow_origin, uint8_t* d_ok, void* stream) {
-    return pipck_verify_packed_bytes_n(d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
-                                       flow_origin, d_ok, nullptr, stream);
+    return launch_packedb(true, d_arena, UINT64_MAX, d_lens, d_tile_off, n, d_pseudo, n_flows, d_flow_of,
+                          flow_origin, nullptr, d_ok, nullptr, as_stream(stream), false);
 }
 
 int pipck_packed_bytes_index(const uint16_t* d_lens, uint64_t n, uint64_t* d_tile_off, void* stream) {

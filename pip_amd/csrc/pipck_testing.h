@@ -53,7 +53,10 @@ extern "C" {
  * row stream k_ring_rx instead of the default k_ring; lanes_per_packet = 256
  * there selects k_ring_slots, loads_per_lane 8 / 24 k_ring's loads in flight,
  * and bits 29 / 27 make k_ring's row stream never / always deal its items
- * round-robin to the block's waves): k_flat (one task per wave)
+ * round-robin to the block's waves -- bit 27 is also the top bit of the small
+ * kernel's depth field below, so set it for ring measurements only; the blocks
+ * argument 8 / 16 / 32 makes that interleaved stream cover so many slots at a
+ * time): k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
  * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
  * for k_flat_coop, bits 8..15 are rows per wave

@@ -304,3 +304,45 @@ def test_chains_bounded_by_arena_segments_and_flows(oracle):
         chain = [host[int(offs[s]):int(offs[s]) + int(seg_lens[s])].tobytes() for s in range(sb[p], sb[p + 1])]
         s, d = oracle.flow4(seed, int(pkt_flow[p]))
         assert got[p] == oracle.inet_checksum_chain(chain, proto, s, d), p
+
+
+@pytest.mark.parametrize("layout", ["bytes", "packed16"])
+@pytest.mark.parametrize("verify", [False, True])
+def test_flow_of_entry_past_the_table_is_an_error(layout, verify):
+    """pipck_*_packed{,_bytes}_n with a per-packet flow table (d_flow_of) and
+    n_flows > 0: an entry >= n_flows (a stale or foreign flow index) gives its
+    packet 0 and sets PIPCK_ERANGE -- pseudo[] is never read there -- while
+    every other packet equals the run with valid entries."""
+    n = 64 * 12 + 5
+    w = CFG4
+    if layout == "bytes":
+        arena, lens, index, _ = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+        fn = "pipck_verify_packed_bytes_n" if verify else "pipck_checksum_packed_bytes_n"
+    else:
+        arena, lens, index, _ = engine.gen_packed(n, 0, w.seed, w.hdr)
+        fn = "pipck_verify_packed_n" if verify else "pipck_checksum_packed_n"
+    pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)[1]
+    rng = np.random.default_rng(3)
+    flows = rng.integers(0, N_FLOWS, n).astype(np.int32)
+    lib = _lib.load()
+
+    def run(fl):
+        d_fl = torch.from_numpy(fl).to("cuda")  # held across the call
+        out = torch.zeros(n, dtype=torch.uint8 if verify else torch.int16, device="cuda")
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        rc = getattr(lib, fn)(_p(arena), C.c_uint64(arena.numel()), _p(lens), _p(index), C.c_uint64(n), _p(pseudo),
+                              C.c_uint32(N_FLOWS), _p(d_fl), C.c_uint64(0), _p(out), _p(err), C.c_void_p(0))
+        torch.cuda.synchronize()
+        assert rc == 0, lib.pipck_last_error()
+        return out.cpu().numpy().view(np.uint8 if verify else np.uint16), int(err.item())
+
+    good, err0 = run(flows)
+    assert err0 == 0
+    bad_at = [0, 63, 64, 400, n - 1]
+    fl2 = flows.copy()
+    fl2[bad_at] = [N_FLOWS, 1 << 30, N_FLOWS + 1, -1, 5000]  # -1: 0xFFFFFFFF as u32
+    got, err = run(fl2)
+    assert err == ERANGE_BIT
+    assert (got[bad_at] == 0).all()
+    keep = np.setdiff1d(np.arange(n), bad_at)
+    assert np.array_equal(got[keep], good[keep])
