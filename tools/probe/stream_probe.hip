@@ -273,6 +273,8 @@ int main(int argc, char** argv) {
         {"pol_sc0_sc1", 32, 4, 64, 46}, {"pol_sc0_sc1_nt", 32, 4, 64, 47},
         // k_packedb's schedule (cfg4): one ~64-row tile per one-wave block, a ring of 32 rows
         {"disp_u32_w1_t64", 32, 1, 64, 0}, {"disp_u32_w1_t128", 32, 1, 128, 0}, {"disp_u24_w1_t64", 24, 1, 64, 0},
+        {"disp_u32_w1_t32", 32, 1, 32, 0}, {"disp_u32_w1_t16", 32, 1, 16, 0}, {"disp_u24_w4_t32", 24, 4, 32, 0},
+        {"disp_u24_w4_t16", 24, 4, 16, 0}, {"disp_u16_w4_t16", 16, 4, 16, 0},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";
