@@ -8,10 +8,11 @@
 // bytes read, every one of them fetched from HBM.  Here nothing but packet
 // bytes (and the 2-byte lengths) is read.
 //
-// k_packedb: one tile of 64 packets per wave, as in k_packed.  The wave reads
-// its 64 u16 lengths and the tile's byte offset (one u64 per tile), derives
-// every packet's offset with a wave prefix scan, and streams the tile as
-// coalesced 1 KiB rows from the 128-B line holding its first byte (rows are
+// k_packedb: one tile of 64 packets per block of W waves (8 by default).  Each
+// wave reads the 64 u16 lengths and the tile's byte offset (one u64 per tile),
+// derives every packet's offset with a wave prefix scan, and the block streams
+// the tile as coalesced 1 KiB rows, wave w taking rows w, w + W, ..., from the
+// 128-B line holding its first byte (rows are
 // whole lines; the bytes before the tile's first packet belong to the
 // previous tile and are summed into a discarded slot).  Since segments are no
 // longer chunk-aligned, a 16-byte chunk may hold the end of one segment and
@@ -33,17 +34,20 @@
 
 namespace pipck {
 
-struct PackedbLds {
+// W = the waves that stream one tile together (rows dealt round-robin)
+template <int W>
+struct PackedbLdsT {
     // +1-encoded segment slots: 0 = the bytes before the tile's first packet,
     // s + 1 = packet s of the tile, nv + 1 .. 65 = bytes after its last packet
     uint32_t end[66];  // end[S] = byte (relative to the line-aligned base) where slot S ends
     uint32_t acc[66];  // LE residue partial per slot
-    uint32_t mark[64];  // (row tag << 7) | S of the slot starting at chunk row + i (max wins)
+    uint32_t mark[W][64];  // per wave: (row tag << 7) | S of the slot starting at chunk row + i (max wins)
 };
 
 // Add a run of whole rows of one slot (per-lane u32 partials in racc) to the
 // slot's LDS partial: one wave sum, one LDS add.
-__device__ __forceinline__ void packedb_flush(PackedbLds& t, int lane, uint32_t& racc, uint32_t& rslot) {
+template <int W>
+__device__ __forceinline__ void packedb_flush(PackedbLdsT<W>& t, int lane, uint32_t& racc, uint32_t& rslot) {
     if (rslot == 0xFFFFFFFFu) return;  // wave-uniform
     const uint32_t tot = wave_total(racc);
     if (lane == 0) atomicAdd(&t.acc[rslot], tot);
@@ -65,8 +69,9 @@ __device__ __forceinline__ void packedb_flush(PackedbLds& t, int lane, uint32_t&
 // k < 6; a chunk holding a packet boundary is window chunk 0 of the packet
 // that starts inside it.  (Tiles with a packet under 16 bytes take the
 // lane-per-segment path and read their headers from memory.)
-template <bool RX>
-__device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, u32x4* hdr, uint32_t row, uint32_t total, int lane,
+template <bool RX, int W>
+__device__ __forceinline__ void packedb_reduce_row(PackedbLdsT<W>& t, uint32_t w, u32x4* hdr, uint32_t row,
+                                                   uint32_t total, int lane,
                                                    const u32x4& v, uint32_t start_v, uint32_t end_v,
                                                    uint32_t mfirst_v, bool valid, uint32_t nv, uint32_t& S0,
                                                    uint32_t& e0, uint32_t& racc, uint32_t& rslot) {
@@ -110,9 +115,9 @@ __device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, u32x4* hdr, ui
     // slot of the chunk's first byte: marks of the packets whose first
     // byte-owned chunk falls in this row, max-scanned from S0 at lane 0
     const uint32_t tag = ((row >> 6) + 1u) << 7;
-    if (valid && mfirst_v > row && mfirst_v < row + 64) atomicMax(&t.mark[mfirst_v - row], tag | (uint32_t)(lane + 1));
+    if (valid && mfirst_v > row && mfirst_v < row + 64) atomicMax(&t.mark[w][mfirst_v - row], tag | (uint32_t)(lane + 1));
     wave_sync();
-    const uint32_t m = t.mark[lane];
+    const uint32_t m = t.mark[w][lane];
     const bool head = lane > 0 && m >= tag;
     const uint32_t S = wave_incl_max(lane == 0 ? S0 : (m >= tag ? (m & 127u) : 0u));
     // bytes of this chunk in slot S: [0, p); the rest [p, 16) opens slot S + 1
@@ -136,10 +141,12 @@ __device__ __forceinline__ void packedb_reduce_row(PackedbLds& t, u32x4* hdr, ui
     (void)nv;
 }
 
-template <int U, bool NT, bool RX>
-__device__ __forceinline__ void packedb_stream(PackedbLds& t, u32x4* hdr, uint32_t total, int lane, uintptr_t base,
-                                               uint32_t start_v, uint32_t end_v, uint32_t mfirst_v, bool valid,
-                                               uint32_t nv) {
+// The tile's 1 KiB rows w, w + W, w + 2W, ... (W = 1: every row), a ring of
+// U rows in flight.
+template <int U, bool NT, bool RX, int W>
+__device__ __forceinline__ void packedb_stream(PackedbLdsT<W>& t, uint32_t w, u32x4* hdr, uint32_t total, int lane,
+                                               uintptr_t base, uint32_t start_v, uint32_t end_v, uint32_t mfirst_v,
+                                               bool valid, uint32_t nv) {
     if (!total) return;
     // the tile's chunks as a range-checked buffer: reads end at the 16-byte
     // boundary after the tile's last byte
@@ -148,19 +155,19 @@ __device__ __forceinline__ void packedb_stream(PackedbLds& t, u32x4* hdr, uint32
     uint32_t S0 = 0, e0 = 0, racc = 0, rslot = 0xFFFFFFFFu;
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        v[u] = buf_load<NT>(tb, (u * 64u + lane) * 16u);
+        v[u] = buf_load<NT>(tb, ((w + W * u) * 64u + lane) * 16u);
         __builtin_amdgcn_sched_barrier(0);  // keep row order
     }
-    for (uint32_t c0 = 0; c0 < total; c0 += 64 * U) {
+    for (uint32_t c0 = 64u * w; c0 < total; c0 += 64 * U * W) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t row = c0 + u * 64;
+            const uint32_t row = c0 + u * 64 * W;
             if (row < total)  // wave-uniform
-                packedb_reduce_row<RX>(t, hdr, row, total, lane, v[u], start_v, end_v, mfirst_v, valid, nv, S0, e0,
-                                       racc, rslot);
+                packedb_reduce_row<RX, W>(t, w, hdr, row, total, lane, v[u], start_v, end_v, mfirst_v, valid, nv, S0,
+                                          e0, racc, rslot);
             // unconditional reload (past the tile: zeros, no request), so each
             // reduce waits for its own row only (vmcnt(U-1))
-            v[u] = buf_load<NT>(tb, (row + 64u * U + lane) * 16u);
+            v[u] = buf_load<NT>(tb, (row + 64u * U * W + lane) * 16u);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -187,14 +194,15 @@ __device__ __forceinline__ uint32_t packedb_lane_sum(uintptr_t base, uint32_t st
 // pipck_rxdev.hip): each frame's sum feeds rx_device_one (pipck_rxparse.hpp) at
 // the tile's end and the ok byte carries the PIPCK_RX_* bits (VERIFY true, no
 // pseudo-header).
-template <bool VERIFY, int U, bool NT, bool RX>
-__device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const uint8_t* __restrict__ arena,
+template <bool VERIFY, int U, bool NT, bool RX, int W>
+__device__ __forceinline__ void packedb_body(PackedbLdsT<W>& t, u32x4* hdr, const uint8_t* __restrict__ arena,
                                              const uint16_t* __restrict__ lens, const uint64_t* __restrict__ tile_off,
                                              uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                              const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
                                              uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
                                              uint64_t arena_bytes, uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
+    const uint32_t w = W > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
     const uint64_t tile = blockIdx.x;
     const uint64_t seg = tile * 64 + lane;
     const bool valid = seg < n;
@@ -216,7 +224,8 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const ui
     const uint64_t toff = tile_off[tile];
     const uint32_t tile_len = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const bool in_arena = toff <= arena_bytes && (uint64_t)tile_len <= arena_bytes - toff;
-    if (!in_arena) {
+    if (!in_arena) {  // (block-uniform: every wave read the same index)
+        if (w != 0) return;
         if (lane == 0 && err) atomicOr(err, 1u << PIPCK_ERANGE);
         if (VERIFY)
             store_result8(buf_rsrc(ok + tile * 64, nv), (uint32_t)lane, 0u);
@@ -231,26 +240,37 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const ui
     const uint32_t end = start + len;
     const uint32_t end_last = (uint32_t)__builtin_amdgcn_readlane((int)end, (int)(nv - 1));
     // slot ends: slot 0 (lead) ends where packet 0 starts; slot s + 1 at packet s's end
-    if (lane == 0) t.end[0] = (uint32_t)(first - base);
-    t.end[lane + 1] = valid ? end : 0xFFFFFFFFu;  // past the last packet: never ends (trailing bytes)
-    if (lane == 0) t.end[65] = 0xFFFFFFFFu;        // (end[64] is lane 63's: a full tile's last packet)
-    t.acc[lane] = 0;
-    if (lane < 2) t.acc[64 + lane] = 0;
-    t.mark[lane] = 0;
-    wave_sync();
+    if (w == 0) {  // (every wave holds the same values; one writes them)
+        if (lane == 0) t.end[0] = (uint32_t)(first - base);
+        t.end[lane + 1] = valid ? end : 0xFFFFFFFFu;  // past the last packet: never ends (trailing bytes)
+        if (lane == 0) t.end[65] = 0xFFFFFFFFu;        // (end[64] is lane 63's: a full tile's last packet)
+        t.acc[lane] = 0;
+        if (lane < 2) t.acc[64 + lane] = 0;
+    }
+    t.mark[w][lane] = 0;
+    if (W > 1)
+        __syncthreads();
+    else
+        wave_sync();
     uint32_t le;
-    const bool lane_path = __any(valid && len < 16);
+    const bool lane_path = __any(valid && len < 16);  // block-uniform
     if (lane_path) {
+        if (w != 0) return;
         le = valid ? packedb_lane_sum(base, start, len) : 0u;
     } else {
         const uint32_t mfirst = (start + 15u) >> 4;  // first chunk whose first byte is in this packet
         const uint32_t total = (end_last + 15u) >> 4;
-        packedb_stream<U, NT, RX>(t, hdr, total, lane, base, start, end, mfirst, valid, nv);
-        wave_sync();
+        packedb_stream<U, NT, RX, W>(t, w, hdr, total, lane, base, start, end, mfirst, valid, nv);
+        if (W > 1) {
+            __syncthreads();  // every wave's rows are in the slot partials
+            if (w != 0) return;  // wave 0 finishes the tile
+        } else {
+            wave_sync();
+        }
         le = t.acc[lane + 1];
     }
-    const uint32_t w = fold16(le);
-    const uint32_t F = (start & 1u) ? w : bswap16(w);  // byte order from the packet's start parity
+    const uint32_t f16 = fold16(le);
+    const uint32_t F = (start & 1u) ? f16 : bswap16(f16);  // byte order from the packet's start parity
     const uint32_t P = pseudo ? Pbase + len : 0u;
     uint32_t r;
     if (RX) {  // the frame's header window: captured from the stream, or (lane path) read again
@@ -279,29 +299,56 @@ __device__ __forceinline__ void packedb_body(PackedbLds& t, u32x4* hdr, const ui
         store_result16(buf_rsrc(out + tile * 64, 2u * nv), 2u * (uint32_t)lane, r);
 }
 
-template <bool VERIFY, int U, bool NT>
-__global__ __launch_bounds__(64) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
-                                                const uint64_t* __restrict__ tile_off, uint64_t n,
-                                                const uint32_t* __restrict__ pseudo, uint32_t n_flows,
-                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                                uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
-                                                uint64_t arena_bytes, uint32_t* __restrict__ err) {
-    __shared__ PackedbLds t;
-    packedb_body<VERIFY, U, NT, false>(t, nullptr, arena, lens, tile_off, n, pseudo, n_flows, flow_of, flow_origin,
-                                       out, ok, arena_bytes, err);
+// W waves stream one tile together, rows dealt round-robin (wave w: rows w,
+// w + W, ...), so a block reads one contiguous window of its tile; slot
+// partials meet in the block's LDS and wave 0 finishes the tile.  W = 8 with a
+// ring of 3 rows is the default (cfg4: 1.151 ms = 0.900 of peak against 1.188
+// ms = 0.873 for one wave per tile with a ring of 32 and 1.173 for 4 waves with
+// a ring of 8, profiles/r05_packedb_waves_ab.jsonl); the loads-only probe of
+// this schedule reached 0.906 (profiles/r05_cfg4_ceiling_probe.jsonl).
+template <bool VERIFY, int U, bool NT, int W>
+__global__ __launch_bounds__(64 * W) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
+                                                    const uint64_t* __restrict__ tile_off, uint64_t n,
+                                                    const uint32_t* __restrict__ pseudo, uint32_t n_flows,
+                                                    const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                                    uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                                    uint64_t arena_bytes, uint32_t* __restrict__ err) {
+    __shared__ PackedbLdsT<W> t;
+    packedb_body<VERIFY, U, NT, false, W>(t, nullptr, arena, lens, tile_off, n, pseudo, n_flows, flow_of,
+                                          flow_origin, out, ok, arena_bytes, err);
 }
 
 // received IP frames: the stream, then each tile's headers parsed and judged
-template <int U, bool NT>
-__global__ __launch_bounds__(64) void k_packedb_rx(const uint8_t* __restrict__ arena,
-                                                   const uint16_t* __restrict__ lens,
-                                                   const uint64_t* __restrict__ tile_off, uint64_t n,
-                                                   uint8_t* __restrict__ ok, uint64_t arena_bytes,
-                                                   uint32_t* __restrict__ err) {
-    __shared__ PackedbLds t;
+template <int U, bool NT, int W>
+__global__ __launch_bounds__(64 * W) void k_packedb_rx(const uint8_t* __restrict__ arena,
+                                                       const uint16_t* __restrict__ lens,
+                                                       const uint64_t* __restrict__ tile_off, uint64_t n,
+                                                       uint8_t* __restrict__ ok, uint64_t arena_bytes,
+                                                       uint32_t* __restrict__ err) {
+    __shared__ PackedbLdsT<W> t;
     __shared__ u32x4 hdr[6 * 64];  // header windows: chunk k of packet s at hdr[k * 64 + s]
-    packedb_body<true, U, NT, true>(t, hdr, arena, lens, tile_off, n, nullptr, 1u, nullptr, 0, nullptr, ok,
-                                    arena_bytes, err);
+    packedb_body<true, U, NT, true, W>(t, hdr, arena, lens, tile_off, n, nullptr, 1u, nullptr, 0, nullptr, ok,
+                                       arena_bytes, err);
+}
+
+// The (W, U) a launch uses, as W * 100 + U.  Internal tune loads_per_lane 32 =
+// one wave per tile with a ring of 32 (the round-4 schedule); 48 = 4 waves,
+// ring 8; 72 / 74 = 8 waves, ring 2 / 4 (k_packedb); 28 = 2 waves, ring 16
+// (k_packedb_rx).  Defaults, from same-box A/Bs
+// (profiles/r05_packedb_waves_ab.jsonl): k_packedb 8 waves with a ring of 3
+// (cfg4 1.147-1.150 ms against 1.188 for one wave); k_packedb_rx 4 waves with a
+// ring of 8 (1.205-1.209 ms against 1.328-1.336 for one wave, 1.259 for 8
+// waves: its tile ends with one wave judging 64 frames, which a narrower block
+// overlaps better).
+static int packedb_shape(bool rx) {
+    switch (g_tune_loads()) {
+        case 32: return 132;
+        case 48: return 408;
+        case 28: return rx ? 216 : 803;
+        case 72: return rx ? 408 : 802;
+        case 74: return rx ? 408 : 804;
+        default: return rx ? 408 : 803;
+    }
 }
 
 // tile_off[t] = bytes of every packet before packet 64 t (the last entry = the
@@ -361,15 +408,26 @@ static int launch_packedb(bool verify, const void* d_arena, uint64_t arena_bytes
     }
     // the kernel's n_flows: the modulus without flow_of; with it, the bound of its entries
     const uint32_t nf = d_flow_of ? (bounded && n_flows ? n_flows : UINT32_MAX) : (n_flows ? n_flows : 1u);
-    // a ring of 32 rows, non-temporal loads, as k_packed
-    if (verify)
-        PIPCK_LAUNCH((k_packedb<true, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
-                          (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
-                          d_ok, arena_bytes, d_err);
-    else
-        PIPCK_LAUNCH((k_packedb<false, 32, true>), dim3((uint32_t)tiles), dim3(64), 0, s,
-                          (const uint8_t*)d_arena, d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out,
-                          d_ok, arena_bytes, d_err);
+    const uint8_t* a = (const uint8_t*)d_arena;
+#define PIPCK_PB(WW, UU)                                                                                       \
+    case WW * 100 + UU:                                                                                        \
+        if (verify)                                                                                            \
+            PIPCK_LAUNCH((k_packedb<true, UU, true, WW>), dim3((uint32_t)tiles), dim3(64 * WW), 0, s, a, d_lens, \
+                         d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, arena_bytes, d_err);  \
+        else                                                                                                   \
+            PIPCK_LAUNCH((k_packedb<false, UU, true, WW>), dim3((uint32_t)tiles), dim3(64 * WW), 0, s, a,        \
+                         d_lens, d_tile_off, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, arena_bytes,   \
+                         d_err);                                                                               \
+        break
+    switch (packedb_shape(false)) {  // non-temporal loads throughout, as k_packed
+        PIPCK_PB(1, 32);
+        PIPCK_PB(4, 8);
+        PIPCK_PB(8, 2);
+        PIPCK_PB(8, 4);
+        default:
+        PIPCK_PB(8, 3);
+    }
+#undef PIPCK_PB
     PIPCK_LAUNCHED("k_packedb");
     return PIPCK_OK;
 }
@@ -392,8 +450,19 @@ int launch_packedb_rx(const void* d_arena, uint64_t arena_bytes, const uint16_t*
         set_error("pipck_rx_verify_device: more than 2^37 packets in one launch");
         return PIPCK_ERANGE;
     }
-    PIPCK_LAUNCH((k_packedb_rx<32, true>), dim3((uint32_t)tiles), dim3(64), 0, s, (const uint8_t*)d_arena, d_lens,
-                 d_tile_off, n, d_ok, arena_bytes, d_err);
+    const uint8_t* a = (const uint8_t*)d_arena;
+#define PIPCK_PBRX(WW, UU)                                                                                     \
+    case WW * 100 + UU:                                                                                        \
+        PIPCK_LAUNCH((k_packedb_rx<UU, true, WW>), dim3((uint32_t)tiles), dim3(64 * WW), 0, s, a, d_lens,       \
+                     d_tile_off, n, d_ok, arena_bytes, d_err);                                                 \
+        break
+    switch (packedb_shape(true)) {
+        PIPCK_PBRX(1, 32);
+        PIPCK_PBRX(2, 16);
+        default:
+        PIPCK_PBRX(4, 8);
+    }
+#undef PIPCK_PBRX
     PIPCK_LAUNCHED("k_packedb_rx");
     return PIPCK_OK;
 }

@@ -1233,13 +1233,29 @@ def _packedb_upload(rng, lens, lead=0):
     return host, offs, arena, lens16, to
 
 
+PACKEDB_SHAPES = {1: 32, 4: 48, 8: 0}  # waves per tile -> tune loads_per_lane (0: the default, 8 waves, ring 3)
+
+
+@pytest.mark.parametrize("tile_waves", [1, 4, 8])
 @pytest.mark.parametrize("shape", ["zipf", "uniform", "tiny", "short", "mixed", "jumbo", "edge", "sixteen"])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 3001])
-def test_packed_bytes_vs_oracle(oracle, shape, n):
+def test_packed_bytes_vs_oracle(oracle, shape, n, tile_waves):
     """Byte-packed batches: segments at every byte alignment (odd starts swap
     pip's byte pairing), chunks split between two segments, rows wholly inside
     one segment, tiles with a segment under 16 bytes (lane-per-segment path),
-    empty segments; implicit / explicit flows and no pseudo-header; RX verify."""
+    empty segments; implicit / explicit flows and no pseudo-header; RX verify.
+    tile_waves: the waves of k_packedb's block streaming one tile (rows dealt
+    round-robin): 8 (the default, a ring of 3), 4 (tune loads_per_lane 48, a
+    ring of 8), 1 (loads_per_lane 32, a ring of 32)."""
+    engine.tune(loads_per_lane=PACKEDB_SHAPES[tile_waves])
+    try:
+        _packed_bytes_vs_oracle(oracle, shape, n, "k_packedb<")
+        assert last_kernel().split("(")[0].endswith(f", {tile_waves}>")
+    finally:
+        engine.tune()
+
+
+def _packed_bytes_vs_oracle(oracle, shape, n, kname):
     rng = np.random.default_rng(hash(("b", shape, n)) % 2**32)
     if shape == "sixteen":  # the smallest lengths the chunk stream takes
         lens = rng.choice([16, 17, 18, 31, 32, 33, 47], n).astype(np.uint32)
@@ -1265,7 +1281,7 @@ def test_packed_bytes_vs_oracle(oracle, shape, n):
             want = oracle.batch_ragged(host, offs, lens, fam, proto, seed, N_FLOWS, origin)
         got = u16(engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, flow_of,
                                                0 if explicit else origin))
-        assert "k_packedb<" in last_kernel()
+        assert kname in last_kernel()
         ok = engine.verify_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, flow_of,
                                         0 if explicit else origin).cpu().numpy().astype(bool)
         assert np.array_equal(got, want), (fam, np.nonzero(got != want)[0][:5])
@@ -1286,6 +1302,33 @@ def test_packed_bytes_equals_packed_on_the_same_packets(oracle):
     assert torch.equal(x, y)
     host, offs, hl = oracle.gen_packed_bytes_batch(w.seed, 5, 3000, w.hdr)
     assert np.array_equal(ab[:len(host)].cpu().numpy()[:int(offs[-1] + hl[-1])], host[:int(offs[-1] + hl[-1])])
+
+
+def test_packedb_shapes_agree_full_size():
+    """cfg4's 8M Zipf batch: k_packedb at every block width and ring depth the
+    launcher has (tune loads_per_lane 32 = one wave, a ring of 32; 48 = 4 waves,
+    a ring of 8; 72 / 0 / 74 = 8 waves, rings of 2 / 3 (the default) / 4) gives
+    the same results, checksums and verify both."""
+    w, n = CFG4, 8 << 20
+    arena, lens16, to, _ = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    engine.tune(loads_per_lane=32)
+    try:
+        want = engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+    finally:
+        engine.tune()
+    shapes = {32: "32, true, 1>", 48: "8, true, 4>", 72: "2, true, 8>", 0: "3, true, 8>", 74: "4, true, 8>"}
+    for lq, tail in shapes.items():
+        engine.tune(loads_per_lane=lq)
+        try:
+            got = engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+            assert last_kernel().split("(")[0].endswith(tail), (lq, last_kernel())
+            ok = engine.verify_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+        finally:
+            engine.tune()
+        assert torch.equal(got, want), lq
+        assert torch.equal(ok.to(torch.bool), want == 0), lq
+    del arena
 
 
 def test_packed_bytes_argument_checks():

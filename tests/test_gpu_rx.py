@@ -116,6 +116,28 @@ def test_rx_verify_c_abi_edges(oracle):
 
 
 # ---- pipck_rx_verify_device: the same packets already in device memory ---------
+
+
+@pytest.fixture(params=[4, 2, 1])
+def tile_waves(request):
+    """k_packedb_rx's block width (waves streaming one tile): 4 is the default
+    (a ring of 8), 2 = tune loads_per_lane 28 (a ring of 16), 1 = 32 (a ring of
+    32); the test checks the launch took it."""
+    from pip_amd import engine
+
+    engine.tune(loads_per_lane={4: 0, 2: 28, 1: 32}[request.param])
+    yield request.param
+    engine.tune()
+
+
+def _rx_kernel_waves():
+    from pip_amd import _lib
+
+    buf = C.create_string_buffer(4096)
+    _lib.check("pipck_last_launch", _lib.load().pipck_last_launch(buf, len(buf)))
+    name = buf.value.decode().split("(")[0]
+    assert "k_packedb_rx<" in name, name
+    return int(name.rsplit(",", 1)[1].rstrip("> "))
 def _device_batch(frames):
     """Frames back to back in a device arena (the byte-packed layout), u16 lengths, tile index."""
     import torch
@@ -143,7 +165,7 @@ def _ipv4(oracle, proto, l4, src=b"\x0a\0\0\x01", dst=b"\x0a\0\0\x02"):
 
 
 @pytest.mark.gpu
-def test_rx_verify_device_equals_host_path(oracle):
+def test_rx_verify_device_equals_host_path(oracle, tile_waves):
     """pipck_rx_verify_device (packets in HBM, parsed on the GPU, payload sums
     derived from the k_packedb stream's frame sums) gives exactly the bits the host-parsed
     pipck_rx_verify gives, on 5,000 oracle-checksummed IPv4/IPv6
@@ -177,13 +199,14 @@ def test_rx_verify_device_equals_host_path(oracle):
         want.append(w)
     arena, lens, tile_off = _device_batch(pkts)
     ok = engine.rx_verify_device(arena, lens, tile_off).cpu().numpy()
+    assert _rx_kernel_waves() == tile_waves
     assert list(ok) == want
     assert (np.array(want) == VERIFIED).sum() > 1000
     torch.cuda.synchronize()
 
 
 @pytest.mark.gpu
-def test_rx_verify_device_edges(oracle):
+def test_rx_verify_device_edges(oracle, tile_waves):
     """Frames the GPU parser must treat as the host parser does: empty, short,
     malformed and non-IP frames; IPv6 extension headers inside and past the
     80-byte register window; fragments and routing headers (unchecked); UDP
@@ -230,11 +253,12 @@ def test_rx_verify_device_edges(oracle):
     keep = [i for i, p in enumerate(frames) if len(p) >= 16]
     arena, lens, tile_off = _device_batch([frames[i] for i in keep])
     dev2 = engine.rx_verify_device(arena, lens, tile_off).cpu().numpy()
+    assert _rx_kernel_waves() == tile_waves
     assert list(dev2) == [host[i] for i in keep]
 
 
 @pytest.mark.gpu
-def test_rx_verify_device_bounded_by_the_arena(oracle):
+def test_rx_verify_device_bounded_by_the_arena(oracle, tile_waves):
     """A tile index that claims more bytes than the arena holds: that tile is
     not read, its packets get 0 and PIPCK_ERANGE is set (no Python guard: the
     C ABI directly)."""
@@ -260,7 +284,7 @@ def test_rx_verify_device_bounded_by_the_arena(oracle):
 
 
 @pytest.mark.gpu
-def test_rx_verify_device_full_size():
+def test_rx_verify_device_full_size(tile_waves):
     """BASELINE scale (8M frames, cfg4's Zipf lengths, 8.5 GB): frames whose
     TCP/UDP and IPv4 header checksums this engine's ragged kernel filled in
     (engine.gen_rx_frames) all verify -- except UDP/IPv4 frames whose checksum
@@ -280,6 +304,7 @@ def test_rx_verify_device_full_size():
     want = torch.full((n,), VERIFIED, dtype=torch.uint8, device="cuda")
     want[no_sum] = UNCHECKED
     ok = engine.rx_verify_device(arena, lens, tile_off)
+    assert _rx_kernel_waves() == tile_waves
     assert torch.equal(ok, want), int((ok != want).sum().item())
     # one byte flipped: an L4 payload byte (not the checksum field) or an IPv4 TTL
     g = torch.Generator(device="cuda").manual_seed(5)

@@ -247,7 +247,7 @@ static void run(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out, ui
 #define PROBE_CASE(u, w) \
     if (m.U == u && m.WPB == w) return launch<u, w>(m, a, rows, out, ctr, cus);
     PROBE_CASE(16, 4) PROBE_CASE(24, 4) PROBE_CASE(32, 4) PROBE_CASE(24, 1) PROBE_CASE(24, 2) PROBE_CASE(24, 8)
-    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8) PROBE_CASE(32, 1)
+    PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8) PROBE_CASE(32, 1) PROBE_CASE(16, 2)
     fprintf(stderr, "no instance U=%d WPB=%d\n", m.U, m.WPB);
     exit(2);
 }
@@ -275,6 +275,9 @@ int main(int argc, char** argv) {
         {"disp_u32_w1_t64", 32, 1, 64, 0}, {"disp_u32_w1_t128", 32, 1, 128, 0}, {"disp_u24_w1_t64", 24, 1, 64, 0},
         {"disp_u32_w1_t32", 32, 1, 32, 0}, {"disp_u32_w1_t16", 32, 1, 16, 0}, {"disp_u24_w4_t32", 24, 4, 32, 0},
         {"disp_u24_w4_t16", 24, 4, 16, 0}, {"disp_u16_w4_t16", 16, 4, 16, 0},
+        // one ~64-row tile per 4-wave block, rows interleaved (a block-interleaved k_packedb)
+        {"coop_u16_w4_t16", 16, 4, 16, 1}, {"coop_u24_w4_t16", 24, 4, 16, 1}, {"coop_u16_w4_t8", 16, 4, 8, 1},
+        {"coop_u16_w2_t32", 16, 2, 32, 1}, {"coop_u24_w2_t32", 24, 2, 32, 1},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";

@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--warm", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--rings", default="ring_sparse_9216,ring_dense_1536,ring_dense_9216,ring_short_2048,ring_short_1024")
-    ap.add_argument("--tune", default="{}", help="engine.tune kwargs for the default (groups) arm, JSON")
+    ap.add_argument("--tune", default="{}", help="engine.tune kwargs for the packed arms and the default (groups) ring arm, JSON")
     ap.add_argument("--skip-packed", action="store_true", help="rings only")
     ap.add_argument("--arms", default="groups,rows,slots",
                     help="ring schedules to time; groups:NAME = the default with --tunes[NAME]")
@@ -89,6 +89,7 @@ def main():
 
     res = {"pass1": [], "rx_verify_device": []}
     kern = {}
+    engine.tune(**tune_default)
     for rnd in range(0 if a.skip_packed else a.rounds):
         for name, fn in (("pass1", pass1), ("rx_verify_device", full)) if rnd % 2 == 0 else \
                 (("rx_verify_device", full), ("pass1", pass1)):
@@ -96,6 +97,7 @@ def main():
                 fn()
             res[name].append(timed_b2b(fn, a.iters))
             kern[name] = last_kernel().split("(")[0]
+    engine.tune()
     # rings: frames in fixed-size slots (pipck_rx_verify_ring), sparse (the same
     # Zipf frames in 9,216-B slots), dense (1,480-B L4 in 1,536-B slots, 8,900-B
     # L4 in 9,216-B slots) and short frames in small slots (200-B L4 in 2 KiB,
