@@ -248,6 +248,7 @@ static void run(const Arm& m, const uint8_t* a, uint64_t rows, uint32_t* out, ui
     if (m.U == u && m.WPB == w) return launch<u, w>(m, a, rows, out, ctr, cus);
     PROBE_CASE(16, 4) PROBE_CASE(24, 4) PROBE_CASE(32, 4) PROBE_CASE(24, 1) PROBE_CASE(24, 2) PROBE_CASE(24, 8)
     PROBE_CASE(16, 8) PROBE_CASE(16, 16) PROBE_CASE(24, 12) PROBE_CASE(32, 8) PROBE_CASE(32, 1) PROBE_CASE(16, 2)
+    PROBE_CASE(2, 8) PROBE_CASE(3, 8) PROBE_CASE(4, 8) PROBE_CASE(4, 4) PROBE_CASE(6, 4) PROBE_CASE(8, 4)
     fprintf(stderr, "no instance U=%d WPB=%d\n", m.U, m.WPB);
     exit(2);
 }
@@ -278,6 +279,10 @@ int main(int argc, char** argv) {
         // one ~64-row tile per 4-wave block, rows interleaved (a block-interleaved k_packedb)
         {"coop_u16_w4_t16", 16, 4, 16, 1}, {"coop_u24_w4_t16", 24, 4, 16, 1}, {"coop_u16_w4_t8", 16, 4, 8, 1},
         {"coop_u16_w2_t32", 16, 2, 32, 1}, {"coop_u24_w2_t32", 24, 2, 32, 1},
+        // shallow rings (k_packedb's round-5 shape: 8 waves x 3 rows on a 64-row tile)
+        {"coop_u3_w8_t8", 3, 8, 8, 1}, {"coop_u3_w8_t32", 3, 8, 32, 1}, {"coop_u3_w8_t64", 3, 8, 64, 1},
+        {"coop_u2_w8_t64", 2, 8, 64, 1}, {"coop_u4_w8_t64", 4, 8, 64, 1}, {"coop_u4_w4_t64", 4, 4, 64, 1},
+        {"coop_u6_w4_t64", 6, 4, 64, 1}, {"coop_u8_w4_t64", 8, 4, 64, 1}, {"coop_u8_w4_t16", 8, 4, 16, 1},
     };
     if (getenv("PROBE_ARMS")) {  // name filter: comma-separated list
         std::string f = std::string(",") + getenv("PROBE_ARMS") + ",";
