@@ -40,6 +40,11 @@ extern "C" {
  * packed ragged tiles always find segments through LDS marks (default: a scalar
  * loop over up to 4 segment ends per row).  The packed-batch kernel
  * (pipck_checksum_packed) takes loads_per_lane 17/25/33 = a ring of 16/24/32.
+ * The byte-packed kernels (pipck_checksum_packed_bytes, k_packedb, default 8
+ * waves per tile with rings of 3; pipck_rx_verify_device, k_packedb_rx,
+ * default 4 waves with rings of 8) take loads_per_lane 32 = one wave per tile
+ * with a ring of 32 (the round-4 shape), 48 = 4 waves x 8, 72 / 74 = 8 waves
+ * x 2 / 4 (k_packedb only), 28 = 2 waves x 16 (k_packedb_rx only).
  * Bit 20 = record the per-task timeline (pipck_trace_tasks below).
  * Bit 21 = MEASUREMENT ONLY, WRONG RESULTS: k_flat waits for and consumes every
  * row with one add and does no per-packet work (times the access pattern
