@@ -106,6 +106,41 @@ def last_kernel() -> str:
     return buf.value.decode()
 
 
+class HipEvents:
+    """n timing events of the HIP runtime torch loaded (the library libpipck
+    launches through), recorded on one stream by raw hipEventRecord."""
+
+    def __init__(self, n: int, stream: int | None):
+        import ctypes as C
+
+        self._C = C
+        self.hip = C.CDLL("libamdhip64.so")
+        self.hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+        self.hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [C.c_void_p]
+        self.stream = C.c_void_p(stream)
+        self.ev = [C.c_void_p() for _ in range(n)]
+        for e in self.ev:
+            if self.hip.hipEventCreate(C.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+        self._rec = self.hip.hipEventRecord
+
+    def record(self, i: int) -> None:
+        if self._rec(self.ev[i], self.stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_s(self, a: int, b: int) -> float:
+        ms = self._C.c_float()
+        if self.hip.hipEventElapsedTime(self._C.byref(ms), self.ev[a], self.ev[b]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value / 1e3
+
+    def destroy(self) -> None:
+        for e in self.ev:
+            self.hip.hipEventDestroy(e)
+        self.ev = []
+
+
 def match_traffic(t: dict, kernel: str, lib_sha: str, algo_bytes: int, stride: int):
     """A PMC traffic record applies to a bench line only if it was measured on the
     same kernel instantiation (full demangled name), the same library build
@@ -199,39 +234,42 @@ def run_rank(args) -> int:
         arena, lens16, tile_off, lens = engine.gen_packed_bytes(count, first, w.seed, w.hdr, lengths=lens)
         l4_bytes = int(lens.to(torch.int64).sum().item())
 
-        def step(out):
-            return engine.checksum_packed_bytes(arena, lens16, tile_off, count, pseudo, N_FLOWS, None, first, out=out)
+        # the C ABI call bound once (pointers, sizes, stream): a step costs the host
+        # what a C caller pays, not this package's per-call argument handling
+        step, out = engine.prepare_checksum_packed_bytes(arena, lens16, tile_off, count, pseudo, N_FLOWS, None, first)
     else:
         first, count = shard.shard_range(n_total, env.world, env.rank)
         arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
         engine.gen_fixed(arena, w.stride, w.length, count, first, w.seed, w.hdr)
         l4_bytes = count * w.length
 
-        def step(out):
-            return engine.checksum_fixed(arena, w.stride, w.length, count, pseudo, N_FLOWS, None, first, out=out)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
+        step, out = engine.prepare_checksum_fixed(arena, w.stride, w.length, count, pseudo, N_FLOWS, None, first)
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step(out)
+        step()
 
-    # an event pair around every launch, on the launch stream (engine launches on
-    # torch's current stream): per-dispatch durations without a profiler
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # a HIP event pair around every launch, on the launch stream (engine launches
+    # on torch's current stream): per-dispatch durations without a profiler.  Raw
+    # hipEventRecord through ctypes: torch.cuda.Event.record costs ~6 us of host
+    # time per event, which on a launch-bound batch (cfg1's 1M headers) is more
+    # than the kernel, and it inflated that kernel's event-pair median from 7.0
+    # to 8.4 us (tools/call_overhead.py, profiles/r05_call_overhead.jsonl)
+    ev = HipEvents(2 * args.steps, engine.current_stream().value)
 
     def timed_step(i):
-        ev_s[i].record()
-        step(out)
-        ev_e[i].record()
+        ev.record(2 * i)
+        step()
+        ev.record(2 * i + 1)
 
     skew = (lambda: time.sleep(env.rank * args.start_skew_ms / 1e3)) if args.start_skew_ms else None
     t0, t1 = shard.timed_steps(env, args.steps, timed_step, torch.cuda.synchronize, before_start=skew)
     kernel = last_kernel()  # the instantiation the timed launches ran
-    per_launch = sorted(s.elapsed_time(e) / 1e3 for s, e in zip(ev_s, ev_e))
+    per_launch = sorted(ev.elapsed_s(2 * i, 2 * i + 1) for i in range(args.steps))
     launch_s = per_launch[len(per_launch) // 2] if args.steps % 2 else \
         (per_launch[args.steps // 2 - 1] + per_launch[args.steps // 2]) / 2
-    b2b_s = ev_s[0].elapsed_time(ev_e[-1]) / 1e3 / args.steps
+    b2b_s = ev.elapsed_s(0, 2 * args.steps - 1) / args.steps
+    ev.destroy()
     ranks = shard.gather_over_ranks(env, [float(l4_bytes), float(count), (t1 - t0) / 1e9, launch_s])
     clocks = shard.gather_ints(env, [t0, t1])
     placements = shard.gather_objects(env, placement)

@@ -15,7 +15,7 @@ from __future__ import annotations
 import ctypes as C
 
 from . import _lib
-from ._lib import Desc, Flow4, Flow6, call, load  # noqa: F401  (re-exported)
+from ._lib import Desc, Flow4, Flow6, call, check, load  # noqa: F401  (re-exported)
 
 DESC_BYTES = C.sizeof(Desc)  # 16: u64 offset, u32 len, u32 flow
 
@@ -93,6 +93,33 @@ def checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows
     call("pipck_checksum_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
          flow_origin, _ptr(out), current_stream(arena.device))
     return out
+
+
+def _bound(fn: str, *args):
+    """A zero-argument call of C entry `fn` with its ctypes arguments built once
+    (pointers, sizes and the stream fixed): what a C caller of the batch ABI
+    pays per batch, without this module's per-call argument handling."""
+    f = getattr(load(), fn)
+
+    def run():
+        rc = f(*args)
+        if rc:
+            check(fn, rc)
+
+    return run
+
+
+def prepare_checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
+                           flow_origin: int = 0, out=None):
+    """checksum_fixed with its arguments checked and bound once; returns (run, out):
+    each run() checksums the batch into out on the current stream.  The tensors
+    must stay alive and in place while run is used."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    _check_span(arena, stride, length, n)
+    return _bound("pipck_checksum_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
+                  flow_origin, _ptr(out), current_stream(arena.device)), out
 
 
 def verify_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
@@ -223,6 +250,20 @@ def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=No
     call("pipck_checksum_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo),
          n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
     return out
+
+
+def prepare_checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1,
+                                  flow_of=None, flow_origin: int = 0, out=None, err=None):
+    """checksum_packed_bytes with its arguments checked and bound once (as
+    prepare_checksum_fixed); returns (run, out)."""
+    torch = _torch()
+    n = lens.numel() if n is None else n
+    if out is None:
+        out = torch.empty(n, dtype=torch.int16, device=arena.device)
+    _check_packed(arena, lens, tile_off, n, unit=1)
+    return _bound("pipck_checksum_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n,
+                  _ptr(pseudo), n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err),
+                  current_stream(arena.device)), out
 
 
 def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
