@@ -130,7 +130,8 @@ def main():
     for (wl, arm), ms in res.items():
         m = statistics.median(ms)
         print(json.dumps({"workload": wl, "packets": meta[wl]["packets"], "arm": arm, "ms": round(m, 4),
-                          "GBps": round(meta[wl]["bytes"] / m / 1e6, 1), "rounds": len(ms)}), flush=True)
+                          "GBps": round(meta[wl]["bytes"] / m / 1e6, 1), "rounds": len(ms),
+                          "rounds_ms": [round(x, 4) for x in ms]}), flush=True)
 
 
 if __name__ == "__main__":
