@@ -1713,3 +1713,30 @@ def test_hdr_in_place_probe_stores_ip_sum(oracle):
     assert np.array_equal(stored, want)
     ok = engine.verify_fixed(arena, w.stride, w.length, n).cpu().numpy()
     assert ok.all()
+
+
+def test_prepared_calls_equal_the_wrappers():
+    """bench.py's step: the C-ABI call bound once (engine.prepare_checksum_fixed /
+    prepare_checksum_packed_bytes) gives the wrappers' results, run after run,
+    and a rebound output is written where the binding says."""
+    w = CFG2
+    n = 5000
+    arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, w.stride, w.length, n, 7, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    want = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 7)
+    run, out = engine.prepare_checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 7)
+    for _ in range(3):
+        out.zero_()
+        run()
+        assert torch.equal(out, want)
+    with pytest.raises(ValueError):  # the span check runs once, at binding
+        engine.prepare_checksum_fixed(arena[:(n - 1) * w.stride + w.length - 1], w.stride, w.length, n)
+    w4 = CFG4
+    ab, lb, to, _ = engine.gen_packed_bytes(3001, 11, w4.seed, w4.hdr)
+    _, p4 = engine.gen_flows(4, N_FLOWS, w4.seed, w4.proto)
+    want = engine.checksum_packed_bytes(ab, lb, to, 3001, p4, N_FLOWS, None, 11)
+    run, out = engine.prepare_checksum_packed_bytes(ab, lb, to, 3001, p4, N_FLOWS, None, 11)
+    run()
+    assert torch.equal(out, want)
+    torch.cuda.synchronize()
