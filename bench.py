@@ -71,6 +71,9 @@ def parse(argv=None):
     p.add_argument("--packets-per-gpu", type=int, default=0, help="override the per-GPU shard size")
     p.add_argument("--cpu-sample", type=int, default=0, help="packets in the CPU-baseline sample (0 = auto)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline and host end-to-end legs")
+    p.add_argument("--results-host", action="store_true",
+                   help="write the 2-B results straight into pinned host memory (where pip consumes them) instead "
+                        "of HBM; the batch stays in HBM; the line says so and carries no PMC traffic figure")
     p.add_argument("--traffic", default="auto",
                    help="JSON with PMC-measured HBM bytes per launch (auto: profiles/traffic_<workload>.json); "
                         "attached only if measured on this exact kernel of this exact libpipck.so build")
@@ -210,6 +213,9 @@ def run_rank(args) -> int:
                  "name": torch.cuda.get_device_name(dev)}
     w = workload(args.workload)
     per_gpu = args.packets_per_gpu or (PER_GPU_PACKETS if w.cfg == 5 else w.n_packets)
+
+    def host_out(count):  # --results-host: the kernel's result stores go to pinned host memory
+        return torch.empty(count, dtype=torch.int16, pin_memory=True) if args.results_host else None
     n_total = per_gpu * env.world
 
     # ---- this rank's shard, generated in HBM from global packet ids
@@ -236,14 +242,16 @@ def run_rank(args) -> int:
 
         # the C ABI call bound once (pointers, sizes, stream): a step costs the host
         # what a C caller pays, not this package's per-call argument handling
-        step, out = engine.prepare_checksum_packed_bytes(arena, lens16, tile_off, count, pseudo, N_FLOWS, None, first)
+        step, out = engine.prepare_checksum_packed_bytes(arena, lens16, tile_off, count, pseudo, N_FLOWS, None, first,
+                                                         out=host_out(count))
     else:
         first, count = shard.shard_range(n_total, env.world, env.rank)
         arena = torch.empty(count * w.stride, dtype=torch.uint8, device="cuda")
         engine.gen_fixed(arena, w.stride, w.length, count, first, w.seed, w.hdr)
         l4_bytes = count * w.length
 
-        step, out = engine.prepare_checksum_fixed(arena, w.stride, w.length, count, pseudo, N_FLOWS, None, first)
+        step, out = engine.prepare_checksum_fixed(arena, w.stride, w.length, count, pseudo, N_FLOWS, None, first,
+                                                  out=host_out(count))
     torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -300,7 +308,9 @@ def run_rank(args) -> int:
     traffic, traffic_src, rocprof_ms = None, "none", None
     sha = lib_sha256()
     tpath = Path(args.traffic) if args.traffic != "auto" else ROOT / "profiles" / f"traffic_cfg{w.cfg}.json"
-    if args.traffic and tpath.exists():
+    if args.results_host:
+        traffic_src = "none (--results-host: the profiles' PMC passes wrote the results to HBM)"
+    elif args.traffic and tpath.exists():
         t = json.loads(tpath.read_text())
         traffic, why = match_traffic(t, kernel, sha, algo_bytes, w.stride)
         traffic_src = f"{tpath.relative_to(ROOT) if tpath.is_relative_to(ROOT) else tpath} ({why})"
@@ -331,6 +341,7 @@ def run_rank(args) -> int:
             "layout": "byte-packed (no padding), u16 lengths + u64 byte offset per 64 packets" if w.ragged
                       else f"fixed {w.stride}-byte slots",
             **({"tune_override": json.loads(args.tune)} if args.tune else {}),
+            "results": "pinned host memory (--results-host)" if args.results_host else "HBM",
             "parallelism": f"{env.world} shard(s), contiguous packet ranges"
                            f"{' of equal bytes' if w.ragged else ''}, no data-path collective"
                            f"{f', {env.world} ranks SHARING {env.world - n_shared} GPU(s) (--share-gpus)' if n_shared else ''}",
