@@ -1740,3 +1740,33 @@ def test_prepared_calls_equal_the_wrappers():
     run()
     assert torch.equal(out, want)
     torch.cuda.synchronize()
+
+
+def test_results_into_pinned_host_memory():
+    """d_out / d_ok may point into pinned host memory (INTEGRATION.md §2,
+    bench.py --results-host): the fixed-stride, byte-packed and verify kernels
+    write there exactly what they write to HBM."""
+    w = CFG2
+    n = 20000
+    arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, w.stride, w.length, n, 3, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    want = engine.checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 3)
+    host = torch.full((n,), -1, dtype=torch.int16, pin_memory=True)
+    run, out = engine.prepare_checksum_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 3, out=host)
+    run()
+    torch.cuda.synchronize()
+    assert out.device.type == "cpu" and torch.equal(out, want.cpu())
+    ok = torch.zeros(n, dtype=torch.uint8, pin_memory=True)
+    engine.verify_fixed(arena, w.stride, w.length, n, pseudo, N_FLOWS, None, 3, ok=ok)
+    torch.cuda.synchronize()
+    assert torch.equal(ok.to(torch.bool), (want == 0).cpu())
+    w4 = CFG4
+    ab, lb, to, _ = engine.gen_packed_bytes(5000, 0, w4.seed, w4.hdr)
+    _, p4 = engine.gen_flows(4, N_FLOWS, w4.seed, w4.proto)
+    want = engine.checksum_packed_bytes(ab, lb, to, 5000, p4, N_FLOWS, None, 0)
+    host = torch.full((5000,), -1, dtype=torch.int16, pin_memory=True)
+    run, out = engine.prepare_checksum_packed_bytes(ab, lb, to, 5000, p4, N_FLOWS, None, 0, out=host)
+    run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, want.cpu())
