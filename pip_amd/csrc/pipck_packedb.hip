@@ -304,8 +304,9 @@ __device__ __forceinline__ void packedb_body(PackedbLdsT<W>& t, u32x4* hdr, cons
 // partials meet in the block's LDS and wave 0 finishes the tile.  W = 8 with a
 // ring of 3 rows is the default (cfg4: 1.151 ms = 0.900 of peak against 1.188
 // ms = 0.873 for one wave per tile with a ring of 32 and 1.173 for 4 waves with
-// a ring of 8, profiles/r05_packedb_waves_ab.jsonl); the loads-only probe of
-// this schedule reached 0.906 (profiles/r05_cfg4_ceiling_probe.jsonl).
+// a ring of 8, profiles/r05_packedb_waves_ab.jsonl), as fast as the loads-only
+// block-interleaved stream over the same bytes (1.147 ms,
+// profiles/r05_cfg4_ceiling_probe.jsonl).
 template <bool VERIFY, int U, bool NT, int W>
 __global__ __launch_bounds__(64 * W) void k_packedb(const uint8_t* __restrict__ arena, const uint16_t* __restrict__ lens,
                                                     const uint64_t* __restrict__ tile_off, uint64_t n,
