@@ -267,6 +267,20 @@ def test_bench_line_names_its_kernel_and_build():
     assert d["per_rank_device"][0]["pci_bus_id"]
 
 
+def test_bench_results_host_line():
+    """`bench.py --results-host`: the kernel writes its results into pinned host
+    memory; the line says so, attaches no PMC traffic (measured with HBM
+    results), and the results still equal pip's own code on the host."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "cfg2", "--steps", "2", "--warmup", "1",
+                        "--packets-per-gpu", "65536", "--results-host"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=_bench_env())
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["config"]["results"].startswith("pinned host memory")
+    assert d["roofline"]["traffic"] is None and "--results-host" in d["roofline"]["traffic_source"]
+    assert d["cpu_baseline"]["gpu_results_match"] is True
+
+
 @pytest.mark.parametrize("launcher", ["self", "torchrun"])
 def test_bench_eight_ranks_rehearsal(launcher):
     """the driver's 8-GPU SCALE line, rehearsed on this box.
