@@ -52,9 +52,11 @@ const char* pipck_last_error(void);
  * header; a minor step only adds entry points).  1.1: the RX verdicts are the
  * 3-bit PIPCK_RX_* values (7 = verified; 3 = nothing failed, payload NOT
  * checked) -- 1.0's single "ok == 3" meant verified.  1.2: the bounded _n forms
- * of the ragged, chain and ring calls. */
+ * of the ragged, chain and ring calls.  1.3: the bounded _n forms of the
+ * fixed-stride calls (pipck_checksum_fixed_n, pipck_verify_fixed_n,
+ * pipck_update_fixed_n). */
 #define PIPCK_VERSION_MAJOR 1
-#define PIPCK_VERSION_MINOR 2
+#define PIPCK_VERSION_MINOR 3
 uint32_t pipck_version(void);
 
 /* ---- flows / pseudo-headers ------------------------------------------ */
@@ -96,6 +98,18 @@ int pipck_flows6_prepare(const pipck_flow6* d_flows, uint32_t n_flows, uint32_t*
 int pipck_checksum_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
                          const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                          uint64_t flow_origin, uint16_t* d_out, void* stream);
+/* Bounded form (replaces the same per-packet calls, pip_checksum.cpp:42-87,
+ * where pip passes the addresses by value -- :42, :63 -- so no index of its
+ * can go stale): with d_pseudo, n_flows must be > 0 (PIPCK_EINVAL otherwise),
+ * and every d_flow_of entry is checked against it on the device.  A packet
+ * whose entry is >= n_flows -- a stale or foreign flow index -- never reads
+ * the pseudo-header table: its result is 0 and d_err (optional, device u32)
+ * is OR-ed with (1 << PIPCK_ERANGE); every other packet's result is unchanged.
+ * The plain name above trusts the entries (n_flows is then unused when
+ * d_flow_of is given). */
+int pipck_checksum_fixed_n(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
+                           const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                           uint64_t flow_origin, uint16_t* d_out, uint32_t* d_err, void* stream);
 
 /* Ragged: one descriptor per packet. */
 typedef struct pipck_desc {
@@ -220,6 +234,10 @@ int pipck_checksum_chains_n(const void* d_arena, uint64_t arena_bytes, const pip
 int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
                        const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
                        uint64_t flow_origin, uint8_t* d_ok, void* stream);
+/* Bounded form, as pipck_checksum_fixed_n: a refused packet verifies as 0. */
+int pipck_verify_fixed_n(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n_packets,
+                         const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of,
+                         uint64_t flow_origin, uint8_t* d_ok, uint32_t* d_err, void* stream);
 /* The same for ragged batches (descriptors as for pipck_checksum_ragged);
  * out-of-domain descriptors verify as 0 and set d_err. */
 int pipck_verify_ragged(const void* d_arena, const pipck_desc* d_desc, uint64_t n_packets,
@@ -247,6 +265,16 @@ int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n_packets, uint3
                        uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new,
                        uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
                        uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, void* stream);
+/* Bounded form: with the pseudo-header tables, n_flows must be > 0 and bounds
+ * every d_flow_of entry on the device.  A packet whose entry is >= n_flows is
+ * left exactly as it was -- its edit bytes are not replaced and its checksum
+ * field is not touched -- and d_err (optional, device u32) is OR-ed with
+ * (1 << PIPCK_ERANGE).  The plain name above trusts the entries. */
+int pipck_update_fixed_n(void* d_arena, uint64_t stride, uint64_t n_packets, uint32_t cover_off, uint32_t cover_len,
+                         uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new,
+                         uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
+                         uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint32_t* d_err,
+                         void* stream);
 
 
 /* ---- synthetic workloads (bench / tests; same spec as oracle/pipck_oracle.c) */

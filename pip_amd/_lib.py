@@ -107,6 +107,10 @@ SIGNATURES = {
     "pipck_checksum_ragged_n": (_i32, [_p, _u64, _p, _u64, _p, _u32, _p, _p, _p]),
     "pipck_verify_ragged_n": (_i32, [_p, _u64, _p, _u64, _p, _u32, _p, _p, _p]),
     "pipck_checksum_chains_n": (_i32, [_p, _u64, _p, _u64, _p, _p, _u64, _p, _u32, _p, _p, _p, _p]),
+    "pipck_checksum_fixed_n": (_i32, [_p, _u64, _u32, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
+    "pipck_verify_fixed_n": (_i32, [_p, _u64, _u32, _u64, _p, _u32, _p, _u64, _p, _p, _p]),
+    "pipck_update_fixed_n": (_i32, [_p, _u64, _u64, _u32, _u32, _u32, _u32, _u32, _p, _u64, _p, _p, _u32, _p, _u64,
+                                    _p, _p]),
 }
 
 # the internal tuning hook (pip_amd/csrc/pipck_testing.h): tests and tools only

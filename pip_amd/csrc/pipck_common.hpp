@@ -85,8 +85,8 @@ int chains_unchecked(const void* d_arena, const pipck_desc* d_segs, uint64_t n_s
 // shape does not fit its block tasks (the caller then takes k_flat).
 int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
                      const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
-                     uint16_t* d_out, uint8_t* d_ok, hipStream_t s, uint32_t rows_per_wave, uint32_t ring,
-                     uint32_t kflags);
+                     uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s, uint32_t rows_per_wave,
+                     uint32_t ring, uint32_t kflags);
 
 // The header row stream (pipck_hdr.hip): 20/24-byte strides, no pseudo-header;
 // PIPCK_EINVAL when the shape does not fit (the caller then takes k_small).

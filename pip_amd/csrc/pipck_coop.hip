@@ -45,7 +45,8 @@ template <int U, bool VERIFY, bool NT, bool PROBE>
 __device__ __forceinline__ void coop_body(uint32_t* s_part, const uint8_t* __restrict__ arena, uint32_t cpp,
                                           uint32_t len, uint64_t n, uint32_t K, const uint32_t* __restrict__ pseudo,
                                           uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                                          uint32_t* __restrict__ err) {
     if (!PROBE) kflags &= ~(kCoopLoadsOnly | kCoopNoEnd);
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -58,11 +59,14 @@ __device__ __forceinline__ void coop_body(uint32_t* s_part, const uint8_t* __res
     const int tail = nch ? (int)len - 16 * ((int)nch - 1) : 16;  // valid bytes of the last data chunk
     for (uint32_t i = threadIdx.x; i < 64u * pitch; i += 256) s_part[i] = 0;
     // pseudo-header base of packet threadIdx.x (K <= 256), loaded now so the
-    // task's end waits on nothing
+    // task's end waits on nothing.  With flow_of, n_flows bounds the entry (the
+    // _n forms; UINT32_MAX: trusted): one past the table is refused at the end.
     uint32_t Pb = 0;
+    bool fbad = false;
     if (pseudo && threadIdx.x < np) {
         const uint64_t pkt = p0 + threadIdx.x;
-        Pb = pseudo[flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows)];
+        Pb = flow_of ? flow_pseudo(pseudo, flow_of[pkt], n_flows, fbad)
+                     : pseudo[(uint32_t)((flow_origin + pkt) % n_flows)];
     }
     __syncthreads();
     const buf_t tb = buf_rsrc(reinterpret_cast<const u32x4*>(arena) + p0 * cpp, tchunks * 16u);
@@ -118,10 +122,11 @@ __device__ __forceinline__ void coop_body(uint32_t* s_part, const uint8_t* __res
         for (int l = 0; l < 64; l++) s += s_part[l * pitch + i];
         const uint32_t F = bswap16(fold16(s));  // packets start 16-byte aligned: even address
         const uint32_t P = pseudo ? Pb + len_term(len) : 0u;
+        if (fbad) flow_refused(err);  // a flow_of entry past the table: result 0
         if (VERIFY)
-            store_result8(buf_rsrc(ok + p0, np), i, (uint32_t)(fold16(P + F) == 0xFFFFu));
+            store_result8(buf_rsrc(ok + p0, np), i, fbad ? 0u : (uint32_t)(fold16(P + F) == 0xFFFFu));
         else
-            store_result16(buf_rsrc(out + p0, 2u * np), 2u * i, finish(P, F));
+            store_result16(buf_rsrc(out + p0, 2u * np), 2u * i, fbad ? 0u : (uint32_t)finish(P, F));
     }
 }
 
@@ -129,10 +134,10 @@ template <int U, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void k_flat_coop(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ err) {
     extern __shared__ uint32_t s_part[];  // 64 lanes x pitch u32 (launch_coop sizes it)
     coop_body<U, VERIFY, NT, false>(s_part, arena, cpp, len, n, K, pseudo, n_flows, flow_of, flow_origin, out, ok,
-                                    kflags);
+                                    kflags, err);
 }
 
 // k_flat_coop with the measurement bits 21 / 22 live (tools only)
@@ -140,23 +145,26 @@ template <int U, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(coop_waves_per_simd<U>()))) void
 k_flat_coop_probe(const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t K,
                   const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of,
-                  uint64_t flow_origin, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                  uint64_t flow_origin, uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                  uint32_t* __restrict__ err) {
     extern __shared__ uint32_t s_part[];
     coop_body<U, VERIFY, NT, true>(s_part, arena, cpp, len, n, K, pseudo, n_flows, flow_of, flow_origin, out, ok,
-                                   kflags);
+                                   kflags, err);
 }
 
 typedef void (*coop_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t, uint32_t*);
 
 // Launch for an aligned arena, 16-B-multiple stride in [1 KiB, 64 KiB], len <=
-// stride (checked by the caller).  rows_per_wave: task size target (0 = auto);
+// stride (checked by the caller); n_flows as launch_fixed hands it to every
+// fixed kernel (the modulus, or with d_flow_of the entries' bound).
+// rows_per_wave: task size target (0 = auto);
 // ring: rows in flight per wave (0 = auto).  Returns PIPCK_OK, or PIPCK_EINVAL
 // when the shape does not fit a block task (the caller then uses k_flat).
 int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
                      const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
-                     uint16_t* d_out, uint8_t* d_ok, hipStream_t s, uint32_t rows_per_wave, uint32_t ring,
-                     uint32_t kflags) {
+                     uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, hipStream_t s, uint32_t rows_per_wave,
+                     uint32_t ring, uint32_t kflags) {
     const uint32_t cpp = (uint32_t)(stride / 16);
     const bool jumbo = cpp >= 256;
     // rows per wave: 64 for jumbo packets (cfg5: 24 packets per block task;
@@ -183,7 +191,7 @@ int launch_flat_coop(bool verify, const void* d_arena, uint64_t stride, uint32_t
     const int ui = u >= 32 ? 2 : (u >= 24 ? 1 : 0);
     const bool probe = (kflags & (kCoopLoadsOnly | kCoopNoEnd)) && !verify;
     PIPCK_LAUNCH(probe ? kCoopProbe[ui] : kCoop[ui][verify], dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, len, n,
-                 K, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, kflags);
+                 K, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, kflags, d_err);
     PIPCK_LAUNCHED("k_flat_coop");
     return PIPCK_OK;
 }

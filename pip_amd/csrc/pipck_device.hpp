@@ -97,6 +97,22 @@ __device__ __forceinline__ uint16_t finish(uint32_t pseudo_total, uint32_t be_su
     return (uint16_t)~fold16(pseudo_total + be_sum);
 }
 
+// Pseudo-header base of a packet whose flow comes from a flow_of entry f.  The
+// fixed-stride kernels get nf = the table's entries in the bounded _n forms
+// (UINT32_MAX in the plain ones: trusted).  pip has no flow index to go stale --
+// it passes the addresses by value on every call (pip_checksum.cpp:42,63) -- so
+// an entry past the table is this engine's own failure mode and must never
+// become a read outside the table: `bad` is set, the table is not read, and the
+// caller stores 0 for that packet and reports it with flow_refused().
+__device__ __forceinline__ uint32_t flow_pseudo(const uint32_t* pseudo, uint32_t f, uint32_t nf, bool& bad) {
+    bad = f >= nf;
+    return bad ? 0u : pseudo[f];
+}
+constexpr uint32_t kErrRange = 1u << 2;  // 1 << PIPCK_ERANGE (include/pipck.h)
+__device__ __forceinline__ void flow_refused(uint32_t* err) {
+    if (err) atomicOr(err, kErrRange);
+}
+
 // Arena loads are issued in the global address space explicitly.  A pointer
 // rebuilt from an integer (the ragged kernel's LDS segment bases) is otherwise
 // generic, and a FLAT load counts against LGKM_CNT as well as VM_CNT: every

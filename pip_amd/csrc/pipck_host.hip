@@ -760,6 +760,16 @@ struct DrainOnError {
             (void)hipStreamSynchronize(c->stream[1]);
         }
     }
+    // The normal end: wait for BOTH streams whatever the first wait returns (a
+    // chunk still queued on stream 1 must not read the caller's input or write
+    // its results after the call has returned), then report the first error.
+    int finish() {
+        const hipError_t e0 = hipStreamSynchronize(c->stream[0]);
+        const hipError_t e1 = hipStreamSynchronize(c->stream[1]);
+        if (e0 != hipSuccess) return hip_fail(e0, "hipStreamSynchronize(stream 0)");
+        if (e1 != hipSuccess) return hip_fail(e1, "hipStreamSynchronize(stream 1)");
+        return PIPCK_OK;
+    }
 };
 
 // Byte-packed host batches (packet i's h_lens[i] bytes right after packet
@@ -803,9 +813,7 @@ int host_packed_chunks(pipck_ctx* c, const void* h_arena, const uint16_t* h_lens
         off += bytes;
     }
     drain.armed = false;
-    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
-    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
-    return PIPCK_OK;
+    return drain.finish();
 }
 
 }  // namespace
@@ -921,9 +929,7 @@ int pipck_host_checksum_fixed(pipck_ctx* c, const void* h_arena, uint64_t stride
         PIPCK_HIP(hipMemcpyAsync(h_out + first, c->d_out[b], m * sizeof(uint16_t), hipMemcpyDeviceToHost, s));
     }
     drain.armed = false;
-    PIPCK_HIP(hipStreamSynchronize(c->stream[0]));
-    PIPCK_HIP(hipStreamSynchronize(c->stream[1]));
-    return PIPCK_OK;
+    return drain.finish();
 }
 
 }  // extern "C"

@@ -45,6 +45,8 @@
 
 namespace pipck {
 
+static_assert(kErrRange == 1u << PIPCK_ERANGE, "pipck_device.hpp's error bit must match include/pipck.h");
+
 // ---------------------------------------------------------------------------
 // flows -> pseudo-header bases
 // ---------------------------------------------------------------------------
@@ -82,7 +84,8 @@ template <int G, int NL, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
                                                uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok) {
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok,
+                                               uint32_t* __restrict__ err) {
     constexpr int GPB = 256 / G;  // packets per block per iteration
     const int sub = threadIdx.x % G;
     uint64_t pkt = (uint64_t)blockIdx.x * GPB + threadIdx.x / G;
@@ -125,11 +128,13 @@ __global__ __launch_bounds__(256) void k_fixed(const uint8_t* __restrict__ arena
         if (sub == 0) {
             const uint32_t F = be_fold(s, addr);
             uint32_t P = 0;
-            if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : flow] + lterm;
+            bool fbad = false;  // a flow_of entry past the table (_n forms): result 0, ERANGE
+            if (pseudo) P = (flow_of ? flow_pseudo(pseudo, flow_of[pkt], n_flows, fbad) : pseudo[flow]) + lterm;
             if (VERIFY)
-                ok[pkt] = fold16(P + F) == 0xFFFFu;
+                ok[pkt] = !fbad && fold16(P + F) == 0xFFFFu;
             else
-                out[pkt] = finish(P, F);
+                out[pkt] = fbad ? (uint16_t)0 : finish(P, F);
+            if (fbad) flow_refused(err);
         }
         if (implicit_flow) {
             flow += flow_step;
@@ -154,12 +159,14 @@ template <int NL, int K, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena, uint64_t stride, uint32_t len,
                                                uint64_t n, const uint32_t* __restrict__ pseudo, uint32_t n_flows,
                                                const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                                               uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                                               uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const uint64_t base = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64u * K);
     if (base >= n) return;  // wave-uniform
     u32x4 v[K][NL];
     uint32_t P[K];
+    uint32_t fbad = 0;  // bit k: packet k's flow_of entry is past the table (_n forms): result 0, ERANGE
     uint32_t flow = 0;
     if (pseudo && !flow_of) flow = (uint32_t)((flow_origin + base + lane) % n_flows);
     const uint32_t fstep = pseudo && !flow_of ? 64u % n_flows : 0u;
@@ -178,7 +185,11 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena
     for (int k = 0; k < K; k++) {
         const uint64_t pkt = base + 64u * k + lane;
         P[k] = 0;
-        if (pseudo && pkt < n) P[k] = pseudo[flow_of ? flow_of[pkt] : flow];
+        if (pseudo && pkt < n) {
+            bool b = false;
+            P[k] = flow_of ? flow_pseudo(pseudo, flow_of[pkt], n_flows, b) : pseudo[flow];
+            fbad |= (uint32_t)b << k;
+        }
         flow += fstep;
         if (flow >= n_flows) flow -= n_flows;
     }
@@ -200,7 +211,9 @@ __global__ __launch_bounds__(256) void k_small(const uint8_t* __restrict__ arena
         }
         const uint32_t F = be_fold(fold64(acc), addr);
         res[k] = VERIFY ? (uint32_t)(fold16(P[k] + lterm + F) == 0xFFFFu) : (uint32_t)finish(P[k] + lterm, F);
+        if ((fbad >> k) & 1u) res[k] = 0;
     }
+    if (fbad) flow_refused(err);
     // Non-temporal result stores.  Results are 2 B per 20-B header here (10 %
     // of the bytes, unlike the streaming kernels' 0.1 %): the write-through sc1
     // policy that the streaming kernels use measured 0.5-1 % slower at 64M-256M
@@ -389,9 +402,11 @@ __device__ __forceinline__ uint32_t flat_flow_of(uint64_t p0, uint32_t np, const
     return pseudo && flow_of && (uint32_t)lane < np ? flow_of[p0 + lane] : 0u;
 }
 __device__ __forceinline__ uint32_t flat_pseudo(uint64_t p0, uint32_t np, const uint32_t* pseudo, uint32_t n_flows,
-                                                const uint32_t* flow_of, uint32_t fo, uint64_t flow_origin, int lane) {
+                                                const uint32_t* flow_of, uint32_t fo, uint64_t flow_origin, int lane,
+                                                bool& fbad) {
+    fbad = false;
     if (!pseudo || (uint32_t)lane >= np) return 0u;
-    if (flow_of) return pseudo[fo];
+    if (flow_of) return flow_pseudo(pseudo, fo, n_flows, fbad);  // n_flows bounds the entry (_n forms)
     const uint64_t f = flow_origin + p0 + (uint64_t)lane;
     // a 32-bit remainder where the index fits (wave-uniform test): the 64-bit one is ~100 instructions
     return pseudo[(flow_origin + p0 + 64u) >> 32 ? (uint32_t)(f % n_flows) : (uint32_t)f % n_flows];
@@ -400,7 +415,7 @@ __device__ __forceinline__ uint32_t flat_pseudo(uint64_t p0, uint32_t np, const 
 template <bool VERIFY, bool TO_LDS = false>
 __device__ __forceinline__ void flat_write(const uint16_t* part, uint32_t pitch, uint64_t p0, uint32_t np,
                                            uint32_t Pb, bool has_pseudo, uint32_t lterm, uint16_t* out, uint8_t* ok,
-                                           int lane, uint32_t kflags, uint64_t magic) {
+                                           int lane, uint32_t kflags, uint64_t magic, bool fbad, uint32_t* err) {
     if ((uint32_t)lane >= np) return;
     uint32_t s = 0;
 #pragma unroll 16
@@ -408,7 +423,11 @@ __device__ __forceinline__ void flat_write(const uint16_t* part, uint32_t pitch,
     const uint32_t F = bswap16(fold16(s));  // packets start 16-byte aligned: even address
     const uint32_t P = has_pseudo ? Pb + lterm : 0u;
     const uint64_t pkt = p0 + lane;
-    const uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    uint32_t r = VERIFY ? (uint32_t)(fold16(P + F) == 0xFFFFu) : (uint32_t)finish(P, F);
+    if (fbad) {  // a flow_of entry past the table: result 0, ERANGE
+        r = 0;
+        flow_refused(err);
+    }
     if (!TO_LDS && (kflags & kEndNoStore) && (uint64_t)r != magic) return;  // measurement: never stores
     if (TO_LDS) {
         out[lane] = (uint16_t)r;  // `out` is this wave's row of the block's LDS results
@@ -517,7 +536,8 @@ template <int U, bool PIPE, bool VERIFY, bool NT, int WPB, bool PROBE, bool XW =
 __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __restrict__ arena, uint32_t cpp,
                                           uint32_t len, uint64_t n, uint32_t run, const uint32_t* __restrict__ pseudo,
                                           uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+                                          uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags,
+                                          uint32_t* __restrict__ err) {
     if (!PROBE) kflags &= ~(kLoadsOnly | kNoTaskEnd | kEndNoStore);
     // the block's place in the task order: its own number, or (XW) its number
     // among the blocks the XCD-weighted deal keeps
@@ -566,7 +586,8 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
         uint32_t acc = 0;  // 16-bit folds (v_dot2_u32_u16): <= 65 chunks of a packet per lane
         RowPos lp{0, 0}, pp{0, 0};
         const uint32_t fo = flat_flow_of(p0, np, pseudo, flow_of, lane);
-        const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, fo, flow_origin, lane);
+        bool fbad;
+        const uint32_t Pb = flat_pseudo(p0, np, pseudo, n_flows, flow_of, fo, flow_origin, lane, fbad);
         u32x4 v[U];
         flat_load_rows<U, NT>(v, tb, 0, lp, cpp, nch, lane);
         if (PIPE && U >= 32) {  // deep ring: one loop, the last batch's reloads are clamped dummies
@@ -614,7 +635,7 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
         if (coalesce && !(kflags & kNoTaskEnd)) {
             const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
             flat_write<VERIFY, true>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, bres + w * run, ok, lane,
-                                     kflags, flow_origin | 0xFFFF000000000000ull);
+                                     kflags, flow_origin | 0xFFFF000000000000ull, fbad, err);
             // release this wave's results, count it in; the last of the block's
             // active waves sees every other wave's results (LDS ops of a wave
             // complete in order; the fences order them against the count)
@@ -647,7 +668,7 @@ __device__ __forceinline__ void flat_body(uint16_t* s_part, const uint8_t* __res
             }
         } else if (!(kflags & kNoTaskEnd)) {
             flat_write<VERIFY>(part, pitch, p0, np, Pb, pseudo != nullptr, lterm, out, ok, lane, kflags,
-                               flow_origin | 0xFFFF000000000000ull);
+                               flow_origin | 0xFFFF000000000000ull, fbad, err);
         }
         trace_task(kflags, trb, task, t_start, lane);
         wave_sync();
@@ -658,10 +679,10 @@ template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ err) {
     extern __shared__ uint16_t s_part[];  // 4 waves x 64 lanes x pitch u16 (launch_fixed sizes it)
     flat_body<U, PIPE, VERIFY, NT, WPB, false>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of, flow_origin,
-                                               out, ok, kflags);
+                                               out, ok, kflags, err);
 }
 
 // k_flat under the XCD-weighted static deal (xw_block; measurement arm, tools only)
@@ -669,10 +690,10 @@ template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_xw(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ err) {
     extern __shared__ uint16_t s_part[];
     flat_body<U, PIPE, VERIFY, NT, WPB, false, true>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of,
-                                                     flow_origin, out, ok, kflags);
+                                                     flow_origin, out, ok, kflags, err);
 }
 
 // k_flat with the measurement bits 21-23 live (tools only)
@@ -680,10 +701,10 @@ template <int U, bool PIPE, bool VERIFY, bool NT, int WPB = 4>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_probe(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ err) {
     extern __shared__ uint16_t s_part[];
     flat_body<U, PIPE, VERIFY, NT, WPB, true>(s_part, arena, cpp, len, n, run, pseudo, n_flows, flow_of, flow_origin,
-                                              out, ok, kflags);
+                                              out, ok, kflags, err);
 }
 
 // ---------------------------------------------------------------------------
@@ -715,7 +736,7 @@ template <int U, bool VERIFY, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_per_simd<U>()))) void k_flat_small(
     const uint8_t* __restrict__ arena, uint32_t cpp, uint32_t len, uint64_t n, uint32_t run,
     const uint32_t* __restrict__ pseudo, uint32_t n_flows, const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
-    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags) {
+    uint16_t* __restrict__ out, uint8_t* __restrict__ ok, uint32_t kflags, uint32_t* __restrict__ err) {
     __shared__ uint32_t s_res[4][kFlatSmallMaxRun];
     const int lane = threadIdx.x & 63;
     uint32_t* res = s_res[threadIdx.x >> 6];
@@ -770,11 +791,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(flat_waves_
             const uint64_t pkt = p0 + i;
             const uint32_t F = bswap16(fold16(res[i]));  // packets start 16-byte aligned: even address
             uint32_t P = 0;
-            if (pseudo) P = pseudo[flow_of ? flow_of[pkt] : flow] + lterm;
+            bool fbad = false;  // a flow_of entry past the table (_n forms): result 0, ERANGE
+            if (pseudo) P = (flow_of ? flow_pseudo(pseudo, flow_of[pkt], n_flows, fbad) : pseudo[flow]) + lterm;
             if (VERIFY)
-                ok[pkt] = fold16(P + F) == 0xFFFFu;
+                ok[pkt] = !fbad && fold16(P + F) == 0xFFFFu;
             else
-                out[pkt] = finish(P, F);
+                out[pkt] = fbad ? (uint16_t)0 : finish(P, F);
+            if (fbad) flow_refused(err);
             flow += fstep;
             if (flow >= n_flows) flow -= n_flows;
         }
@@ -825,7 +848,8 @@ __global__ __launch_bounds__(256) void k_flat_tiny(const uint8_t* __restrict__ a
                                                    uint64_t n, uint32_t run, const uint32_t* __restrict__ pseudo,
                                                    uint32_t n_flows, const uint32_t* __restrict__ flow_of,
                                                    uint64_t flow_origin, uint16_t* __restrict__ out,
-                                                   uint8_t* __restrict__ ok, uint32_t kflags) {
+                                                   uint8_t* __restrict__ ok, uint32_t kflags,
+                                                   uint32_t* __restrict__ err) {
     extern __shared__ uint32_t s_tiny[];  // 4 waves x tiny_wave_lds(hpp, run) bytes (launch_fixed sizes it)
     const int lane = threadIdx.x & 63;
     const uint32_t stride = 8u * hpp;
@@ -886,7 +910,12 @@ __global__ __launch_bounds__(256) void k_flat_tiny(const uint8_t* __restrict__ a
         auto result = [&](uint32_t i, uint32_t flow) -> uint32_t {
             const uint32_t F = fs[i];
             uint32_t P_ = 0;
-            if (pseudo) P_ = pseudo[flow_of ? flow_of[p0 + i] : flow] + lterm;
+            bool fbad = false;  // a flow_of entry past the table (_n forms): result 0, ERANGE
+            if (pseudo) P_ = (flow_of ? flow_pseudo(pseudo, flow_of[p0 + i], n_flows, fbad) : pseudo[flow]) + lterm;
+            if (fbad) {
+                flow_refused(err);
+                return 0u;
+            }
             return VERIFY ? (uint32_t)(fold16(P_ + F) == 0xFFFFu) : (uint32_t)finish(P_, F);
         };
         const bool vec = ((VERIFY ? (uintptr_t)ok : (uintptr_t)out) & (VERIFY ? 3u : 7u)) == 0;  // p0 % 64 == 0
@@ -1465,7 +1494,7 @@ std::atomic<uint32_t> g_probes{0};  // pipck_tune_probes (pipck_testing.h)
 thread_local const void* t_last_kernel = nullptr;
 
 typedef void (*fixed_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
-                         uint64_t, uint16_t*, uint8_t*);
+                         uint64_t, uint16_t*, uint8_t*, uint32_t*);
 struct Variant {
     int g, nl;
     fixed_fn fn[2][2];  // [verify][nt]
@@ -1516,7 +1545,7 @@ static const Variant& pick_variant(uint32_t nch) {
 
 constexpr uint32_t kNoSmall = 64u;  // pipck_tune flags bit 6: never the small-packet kernel
 typedef void (*small_fn)(const uint8_t*, uint64_t, uint32_t, uint64_t, const uint32_t*, uint32_t, const uint32_t*,
-                         uint64_t, uint16_t*, uint8_t*, uint32_t);
+                         uint64_t, uint16_t*, uint8_t*, uint32_t, uint32_t*);
 struct SmallVariant {
     int k;              // packets per lane per wave task
     small_fn fn[4][2][2];  // [nl-1][verify][nt]
@@ -1549,7 +1578,7 @@ static std::atomic<uint32_t> g_xw_kept{0}, g_xw_period{0};
 static bool flat_allowed() { return (g_tune.flags.load() & 2u) == 0; }  // bit 1: never the flat kernel
 
 typedef void (*flat_fn)(const uint8_t*, uint32_t, uint32_t, uint64_t, uint32_t, const uint32_t*, uint32_t,
-                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t);
+                        const uint32_t*, uint64_t, uint16_t*, uint8_t*, uint32_t, uint32_t*);
 struct FlatVariant {
     int u;
     bool pipe;
@@ -1620,9 +1649,12 @@ static bool nt_for(bool streaming) {
     return streaming;
 }
 
+// bounded: the _n forms (n_flows > 0 with d_pseudo; it bounds every d_flow_of
+// entry on the device, d_err reports a refused one); the plain forms trust the
+// entries and ignore n_flows when d_flow_of is given
 static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint32_t len, uint64_t n,
                         const uint32_t* d_pseudo, uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin,
-                        uint16_t* d_out, uint8_t* d_ok, void* stream) {
+                        uint16_t* d_out, uint8_t* d_ok, uint32_t* d_err, void* stream, bool bounded) {
     if (n == 0) return PIPCK_OK;
     if (!d_arena || (verify ? !d_ok : !d_out)) {
         set_error("pipck_checksum_fixed: null arena/output");
@@ -1632,17 +1664,19 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         set_error("pipck_checksum_fixed: len > 65535 is outside the batch domain");
         return PIPCK_ERANGE;
     }
-    if (d_pseudo && !d_flow_of && n_flows == 0) {
+    if (d_pseudo && (bounded || !d_flow_of) && n_flows == 0) {
         set_error("pipck_checksum_fixed: n_flows == 0");
         return PIPCK_EINVAL;
     }
+    // the kernels' n_flows: the modulus without flow_of; with it, the bound of its entries
+    const uint32_t nf = d_flow_of ? (bounded ? n_flows : UINT32_MAX) : (n_flows ? n_flows : 1u);
     if (stride < len && n > 1) {
         set_error("pipck_checksum_fixed: stride < len");
         return PIPCK_EINVAL;
     }
     if (g_tune.lanes.load() == kWaveArm)  // measurement arm: one packet per wave (pipck_wave.hip)
-        return launch_wave(verify, false, d_arena, stride, len, nullptr, n, d_pseudo, n_flows, d_flow_of, flow_origin,
-                           d_out, d_ok, nullptr, as_stream(stream), (len + 30u) / 16u, g_tune.loads.load());
+        return launch_wave(verify, false, d_arena, stride, len, nullptr, n, d_pseudo, nf, d_flow_of, flow_origin,
+                           d_out, d_ok, d_err, as_stream(stream), (len + 30u) / 16u, g_tune.loads.load());
     const bool aligned = ((uintptr_t)d_arena % 16 == 0) && (stride % 16 == 0);
     if (aligned && flat_allowed() && !g_tune.lanes.load() && stride >= 64 * 16 && stride <= (1ull << 24) &&
         len <= stride) {
@@ -1661,8 +1695,8 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         // is tune bit 28; strides past 64 KiB always take k_flat.
         const bool coop = (stride != 1024 && stride != 2048) != ((g_tune.flags.load() & kFlatAltSchedule) != 0);
         if (coop && stride <= 65536 &&
-            launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, d_ok,
-                             as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load(),
+            launch_flat_coop(verify, d_arena, stride, len, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok,
+                             d_err, as_stream(stream), (g_tune.flags.load() >> 8) & 0xFFu, g_tune.loads.load(),
                              g_tune.flags.load()) == PIPCK_OK)
             return PIPCK_OK;
         // Rows in flight per wave and task size.  Jumbo packets (>= 4 KiB, cfg3
@@ -1696,13 +1730,13 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
             const uint64_t P = 8ull * g_xw_period.load(), periods = (grid + xa - 1) / xa;
             PIPCK_LAUNCH((k_flat_xw<24, true, false, true>), dim3((uint32_t)(periods * P)), dim3(256), lds,
                          as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
-                         n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+                         nf, d_flow_of, flow_origin, d_out, d_ok, flags, d_err);
             PIPCK_LAUNCHED("k_flat_xw");
             return PIPCK_OK;
         }
         PIPCK_LAUNCH(probe ? fv->probe : fv->fn[verify][nt_for(true)], dim3(grid), dim3(256), lds, as_stream(stream),
-                           (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, n_flows ? n_flows : 1u, d_flow_of,
-                           flow_origin, d_out, d_ok, flags);
+                           (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo, nf, d_flow_of,
+                           flow_origin, d_out, d_ok, flags, d_err);
         PIPCK_LAUNCHED("k_flat");
         return PIPCK_OK;
     }
@@ -1719,7 +1753,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint64_t tasks = (n + run - 1) / run;
         PIPCK_LAUNCH(kFlatSmall[verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), 0,
                            as_stream(stream), (const uint8_t*)d_arena, cpp, len, n, run, d_pseudo,
-                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+                           nf, d_flow_of, flow_origin, d_out, d_ok, flags, d_err);
         PIPCK_LAUNCHED("k_flat_small");
         return PIPCK_OK;
     }
@@ -1763,7 +1797,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const size_t lds = 4u * tiny_wave_lds(hpp, run);
         PIPCK_LAUNCH(kFlatTiny[ui][verify][nt_for(true)], dim3(grid_for(4, tasks, 0)), dim3(256), lds,
                            as_stream(stream), (const uint8_t*)d_arena, hpp, len, n, run, d_pseudo,
-                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, flags);
+                           nf, d_flow_of, flow_origin, d_out, d_ok, flags, d_err);
         PIPCK_LAUNCHED("k_flat_tiny");
         return PIPCK_OK;
     }
@@ -1778,7 +1812,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
         const uint64_t waves = (n + 64u * sv.k - 1) / (64u * sv.k);
         PIPCK_LAUNCH(sv.fn[small_nl ? small_nl - 1 : 0][verify][nt_for(false)], dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0,
                            as_stream(stream), (const uint8_t*)d_arena, stride, len, n, d_pseudo,
-                           n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok, g_tune.flags.load());
+                           nf, d_flow_of, flow_origin, d_out, d_ok, g_tune.flags.load(), d_err);
         PIPCK_LAUNCHED("k_small");
         return PIPCK_OK;
     }
@@ -1786,7 +1820,7 @@ static int launch_fixed(bool verify, const void* d_arena, uint64_t stride, uint3
     const Variant& v = pick_variant(nch);
     const uint32_t grid = grid_for(256 / v.g, n);
     PIPCK_LAUNCH(v.fn[verify][nt_for(false)], dim3(grid), dim3(256), 0, as_stream(stream), (const uint8_t*)d_arena,
-                       stride, len, n, d_pseudo, n_flows ? n_flows : 1u, d_flow_of, flow_origin, d_out, d_ok);
+                       stride, len, n, d_pseudo, nf, d_flow_of, flow_origin, d_out, d_ok, d_err);
     PIPCK_LAUNCHED("k_fixed");
     return PIPCK_OK;
 }
@@ -2038,18 +2072,33 @@ int pipck_flows6_prepare(const pipck_flow6* d_flows, uint32_t n, uint32_t* d_pse
     return PIPCK_OK;
 }
 
+int pipck_checksum_fixed_n(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
+                           uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
+                           uint32_t* d_err, void* stream) {
+    return launch_fixed(false, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, nullptr,
+                        d_err, stream, true);
+}
+
+int pipck_verify_fixed_n(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
+                         uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok,
+                         uint32_t* d_err, void* stream) {
+    return launch_fixed(true, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr, d_ok,
+                        d_err, stream, true);
+}
+
+// the unbounded forms (flow_of entries trusted, n_flows unused with them)
 int pipck_checksum_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
                          uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint16_t* d_out,
                          void* stream) {
     return launch_fixed(false, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, d_out, nullptr,
-                        stream);
+                        nullptr, stream, false);
 }
 
 int pipck_verify_fixed(const void* d_arena, uint64_t stride, uint32_t len, uint64_t n, const uint32_t* d_pseudo,
                        uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, uint8_t* d_ok,
                        void* stream) {
     return launch_fixed(true, d_arena, stride, len, n, d_pseudo, n_flows, d_flow_of, flow_origin, nullptr, d_ok,
-                        stream);
+                        nullptr, stream, false);
 }
 
 int pipck_checksum_ragged_n(const void* d_arena, uint64_t arena_bytes, const pipck_desc* d_desc, uint64_t n,

@@ -40,7 +40,8 @@ __global__ __launch_bounds__(256) void k_update_fixed(uint8_t* __restrict__ aren
                                                       const uint8_t* __restrict__ nb, uint64_t new_stride,
                                                       const uint32_t* __restrict__ pseudo_old,
                                                       const uint32_t* __restrict__ pseudo_new, uint32_t n_flows,
-                                                      const uint32_t* __restrict__ flow_of, uint64_t flow_origin) {
+                                                      const uint32_t* __restrict__ flow_of, uint64_t flow_origin,
+                                                      uint32_t* __restrict__ err) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint8_t* a = arena + i * stride;
@@ -48,6 +49,15 @@ __global__ __launch_bounds__(256) void k_update_fixed(uint8_t* __restrict__ aren
     uint32_t po = 0, pn = 0;
     if (pseudo_old) {
         const uint32_t f = flow_of ? flow_of[i] : (uint32_t)((flow_origin + i) % n_flows);
+        // with flow_of, n_flows bounds the entry (pipck_update_fixed_n; UINT32_MAX:
+        // trusted).  A stale entry must not turn into a checksum computed from
+        // bytes outside the tables and written into the packet: the packet is
+        // left exactly as it was -- edit bytes and checksum field -- and the
+        // call reports PIPCK_ERANGE.
+        if (flow_of && f >= n_flows) {
+            flow_refused(err);
+            return;
+        }
         po = pseudo_old[f];
         pn = pseudo_new[f];
     }
@@ -80,16 +90,16 @@ __global__ __launch_bounds__(256) void k_update_fixed(uint8_t* __restrict__ aren
 
 using namespace pipck;
 
-extern "C" int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n, uint32_t cover_off, uint32_t cover_len,
-                                  uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new,
-                                  uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
-                                  uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, void* stream) {
+static int update_fixed(void* d_arena, uint64_t stride, uint64_t n, uint32_t cover_off, uint32_t cover_len,
+                        uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new, uint64_t new_stride,
+                        const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new, uint32_t n_flows,
+                        const uint32_t* d_flow_of, uint64_t flow_origin, uint32_t* d_err, void* stream, bool bounded) {
     if (n == 0) return PIPCK_OK;
     const uint64_t cover_end = (uint64_t)cover_off + cover_len, edit_end = (uint64_t)edit_off + edit_len;
     const char* why = nullptr;
     if (!d_arena || (edit_len && !d_new)) why = "null arena/new bytes";
     else if ((d_pseudo_old == nullptr) != (d_pseudo_new == nullptr)) why = "pseudo_old and pseudo_new must both be set or both NULL";
-    else if (d_pseudo_old && n_flows == 0 && !d_flow_of) why = "n_flows == 0";
+    else if (d_pseudo_old && n_flows == 0 && (bounded || !d_flow_of)) why = "n_flows == 0";
     else if (cover_len > PIPCK_MAX_SEG_LEN) why = "cover_len > 65535 is outside the batch domain";
     else if (ck_off < cover_off || (uint64_t)ck_off + 2 > cover_end || ((ck_off - cover_off) & 1))
         why = "checksum field must be an even-offset word inside the cover";
@@ -102,10 +112,34 @@ extern "C" int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n, ui
         set_error(std::string("pipck_update_fixed: ") + why);
         return PIPCK_EINVAL;
     }
+    if ((n + 255) / 256 > 0x7FFFFFFFull) {
+        set_error("pipck_update_fixed: too many packets for one launch");
+        return PIPCK_ERANGE;
+    }
+    // the kernel's n_flows: the modulus without flow_of; with it, the bound of its entries
+    const uint32_t nf = d_flow_of ? (bounded ? n_flows : UINT32_MAX) : n_flows;
     hipLaunchKernelGGL(k_update_fixed, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
                        (uint8_t*)d_arena, stride, n, cover_off, cover_len, ck_off, edit_off, edit_len,
-                       (const uint8_t*)d_new, new_stride, d_pseudo_old, d_pseudo_new, n_flows, d_flow_of,
-                       flow_origin);
+                       (const uint8_t*)d_new, new_stride, d_pseudo_old, d_pseudo_new, nf, d_flow_of,
+                       flow_origin, d_err);
     PIPCK_LAUNCHED("k_update_fixed");
     return PIPCK_OK;
+}
+
+extern "C" int pipck_update_fixed_n(void* d_arena, uint64_t stride, uint64_t n, uint32_t cover_off,
+                                    uint32_t cover_len, uint32_t ck_off, uint32_t edit_off, uint32_t edit_len,
+                                    const void* d_new, uint64_t new_stride, const uint32_t* d_pseudo_old,
+                                    const uint32_t* d_pseudo_new, uint32_t n_flows, const uint32_t* d_flow_of,
+                                    uint64_t flow_origin, uint32_t* d_err, void* stream) {
+    return update_fixed(d_arena, stride, n, cover_off, cover_len, ck_off, edit_off, edit_len, d_new, new_stride,
+                        d_pseudo_old, d_pseudo_new, n_flows, d_flow_of, flow_origin, d_err, stream, true);
+}
+
+// the unbounded form (flow_of entries trusted, n_flows unused with them)
+extern "C" int pipck_update_fixed(void* d_arena, uint64_t stride, uint64_t n, uint32_t cover_off, uint32_t cover_len,
+                                  uint32_t ck_off, uint32_t edit_off, uint32_t edit_len, const void* d_new,
+                                  uint64_t new_stride, const uint32_t* d_pseudo_old, const uint32_t* d_pseudo_new,
+                                  uint32_t n_flows, const uint32_t* d_flow_of, uint64_t flow_origin, void* stream) {
+    return update_fixed(d_arena, stride, n, cover_off, cover_len, ck_off, edit_off, edit_len, d_new, new_stride,
+                        d_pseudo_old, d_pseudo_new, n_flows, d_flow_of, flow_origin, nullptr, stream, false);
 }

@@ -52,6 +52,9 @@ __global__ __launch_bounds__(256) void k_wave(const uint8_t* __restrict__ arena,
         off = pkt * stride;
         L = len;
         if (pseudo) flow = flow_of ? flow_of[pkt] : (uint32_t)((flow_origin + pkt) % n_flows);
+        // a flow_of entry past the table (n_flows bounds it in the _n forms): result 0
+        bad = pseudo && flow_of && flow >= n_flows;
+        if (bad) L = 0, flow = 0;
     }
     const uint32_t Pb = pseudo ? pseudo[flow] : 0u;  // issued before the payload: ready at the end
     const uintptr_t addr = (uintptr_t)arena + off;

@@ -84,14 +84,30 @@ def flows_to_device(family: int, flows_bytes: bytes, device=None):
 
 
 # ---------------------------------------------------------------- batches
-def checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
-                   flow_origin: int = 0, out=None):
+def _n_flows(n_flows, pseudo, flow_of) -> int:
+    """The n_flows a bounded (_n) call gets.  Without flow_of it is the modulus of
+    (flow_origin + i) % n_flows (default 1); with flow_of it bounds every entry on
+    the device (an entry >= n_flows gives that packet 0 and PIPCK_ERANGE), so its
+    default is the whole table, pseudo.numel() -- never 1, which would refuse every
+    packet whose flow is >= 1."""
+    if n_flows is not None:
+        return n_flows
+    if flow_of is not None and pseudo is not None:
+        return pseudo.numel()
+    return 1
+
+
+def checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int | None = None, flow_of=None,
+                   flow_origin: int = 0, out=None, err=None):
+    """Fixed-stride batch (pipck_checksum_fixed_n): packet i at arena[i * stride:], `length` bytes.
+    flow_of entries are bounded on the device by n_flows (default: the whole pseudo table); an
+    entry past it gives that packet 0 and ORs 1 << PIPCK_ERANGE into err (optional device int32)."""
     torch = _torch()
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_span(arena, stride, length, n)
-    call("pipck_checksum_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
-         flow_origin, _ptr(out), current_stream(arena.device))
+    call("pipck_checksum_fixed_n", _ptr(arena), stride, length, n, _ptr(pseudo), _n_flows(n_flows, pseudo, flow_of),
+         _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
     return out
 
 
@@ -109,8 +125,8 @@ def _bound(fn: str, *args):
     return run
 
 
-def prepare_checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
-                           flow_origin: int = 0, out=None):
+def prepare_checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int | None = None,
+                           flow_of=None, flow_origin: int = 0, out=None, err=None):
     """checksum_fixed with its arguments checked and bound once; returns (run, out):
     each run() checksums the batch into out on the current stream.  The tensors
     must stay alive and in place while run is used."""
@@ -118,18 +134,21 @@ def prepare_checksum_fixed(arena, stride: int, length: int, n: int, pseudo=None,
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_span(arena, stride, length, n)
-    return _bound("pipck_checksum_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
-                  flow_origin, _ptr(out), current_stream(arena.device)), out
+    return _bound("pipck_checksum_fixed_n", _ptr(arena), stride, length, n, _ptr(pseudo),
+                  _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(out), _ptr(err),
+                  current_stream(arena.device)), out
 
 
-def verify_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int = 1, flow_of=None,
-                 flow_origin: int = 0, ok=None):
+def verify_fixed(arena, stride: int, length: int, n: int, pseudo=None, n_flows: int | None = None, flow_of=None,
+                 flow_origin: int = 0, ok=None, err=None):
+    """RX verification of a fixed-stride batch (pipck_verify_fixed_n, bounded as checksum_fixed:
+    a refused packet verifies as 0)."""
     torch = _torch()
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
     _check_span(arena, stride, length, n)
-    call("pipck_verify_fixed", _ptr(arena), stride, length, n, _ptr(pseudo), n_flows, _ptr(flow_of),
-         flow_origin, _ptr(ok), current_stream(arena.device))
+    call("pipck_verify_fixed_n", _ptr(arena), stride, length, n, _ptr(pseudo), _n_flows(n_flows, pseudo, flow_of),
+         _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err), current_stream(arena.device))
     return ok
 
 
@@ -169,31 +188,34 @@ def _nbytes(t) -> int:
     return t.numel() * t.element_size()
 
 
-def checksum_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                    flow_origin: int = 0, out=None, err=None):
+def checksum_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int | None = None,
+                    flow_of=None, flow_origin: int = 0, out=None, err=None):
     """Packed ragged batch (pipck_checksum_packed_n): lens = device int16/uint16 tensor of
     packet lengths, tile_chunk = packed_index(lens); packet i at 16 * (chunks before i).
     The device bounds every tile by the arena's size (err: optional device int32,
-    OR-ed with 1 << PIPCK_ERANGE for a tile past it, whose results are then 0)."""
+    OR-ed with 1 << PIPCK_ERANGE for a tile past it, whose results are then 0) and
+    every flow_of entry by n_flows (default: the whole pseudo table, as _n_flows)."""
     torch = _torch()
     n = lens.numel() if n is None else n
     if out is None:
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_packed(arena, lens, tile_chunk, n)
     call("pipck_checksum_packed_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo),
-         n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
+         _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(out), _ptr(err),
+         current_stream(arena.device))
     return out
 
 
-def verify_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                  flow_origin: int = 0, ok=None, err=None):
+def verify_packed(arena, lens, tile_chunk, n: int | None = None, pseudo=None, n_flows: int | None = None,
+                  flow_of=None, flow_origin: int = 0, ok=None, err=None):
     torch = _torch()
     n = lens.numel() if n is None else n
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
     _check_packed(arena, lens, tile_chunk, n)
     call("pipck_verify_packed_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_chunk), n, _ptr(pseudo),
-         n_flows, _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err), current_stream(arena.device))
+         _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err),
+         current_stream(arena.device))
     return ok
 
 
@@ -237,8 +259,8 @@ def _check_packed(arena, lens, tile_chunk, n, unit: int = 16):
         raise ValueError(f"packed batch needs {need} B, arena has {arena.numel() * arena.element_size()}")
 
 
-def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                          flow_origin: int = 0, out=None, err=None):
+def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int | None = None,
+                          flow_of=None, flow_origin: int = 0, out=None, err=None):
     """Byte-packed ragged batch (pipck_checksum_packed_bytes_n): packets back to back with no padding,
     lens = device int16/uint16 lengths, tile_off = packed_bytes_index(lens); arena 128-byte aligned.
     Tiles are bounded by the arena's size on the device (err as checksum_packed)."""
@@ -248,12 +270,13 @@ def checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=No
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_packed(arena, lens, tile_off, n, unit=1)
     call("pipck_checksum_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo),
-         n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err), current_stream(arena.device))
+         _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(out), _ptr(err),
+         current_stream(arena.device))
     return out
 
 
-def prepare_checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1,
-                                  flow_of=None, flow_origin: int = 0, out=None, err=None):
+def prepare_checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None,
+                                  n_flows: int | None = None, flow_of=None, flow_origin: int = 0, out=None, err=None):
     """checksum_packed_bytes with its arguments checked and bound once (as
     prepare_checksum_fixed); returns (run, out)."""
     torch = _torch()
@@ -262,19 +285,20 @@ def prepare_checksum_packed_bytes(arena, lens, tile_off, n: int | None = None, p
         out = torch.empty(n, dtype=torch.int16, device=arena.device)
     _check_packed(arena, lens, tile_off, n, unit=1)
     return _bound("pipck_checksum_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n,
-                  _ptr(pseudo), n_flows, _ptr(flow_of), flow_origin, _ptr(out), _ptr(err),
-                  current_stream(arena.device)), out
+                  _ptr(pseudo), _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(out),
+                  _ptr(err), current_stream(arena.device)), out
 
 
-def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int = 1, flow_of=None,
-                        flow_origin: int = 0, ok=None, err=None):
+def verify_packed_bytes(arena, lens, tile_off, n: int | None = None, pseudo=None, n_flows: int | None = None,
+                        flow_of=None, flow_origin: int = 0, ok=None, err=None):
     torch = _torch()
     n = lens.numel() if n is None else n
     if ok is None:
         ok = torch.empty(n, dtype=torch.uint8, device=arena.device)
     _check_packed(arena, lens, tile_off, n, unit=1)
     call("pipck_verify_packed_bytes_n", _ptr(arena), _nbytes(arena), _ptr(lens), _ptr(tile_off), n, _ptr(pseudo),
-         n_flows, _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err), current_stream(arena.device))
+         _n_flows(n_flows, pseudo, flow_of), _ptr(flow_of), flow_origin, _ptr(ok), _ptr(err),
+         current_stream(arena.device))
     return ok
 
 
@@ -333,16 +357,20 @@ def checksum_chains(arena, segs, seg_begin, pkt_flow=None, pseudo=None, out=None
 
 def update_fixed(arena, stride: int, n: int, cover_off: int, cover_len: int, ck_off: int, edit_off: int,
                  edit_len: int, new_bytes=None, new_stride: int = 0, pseudo_old=None, pseudo_new=None,
-                 n_flows: int = 1, flow_of=None, flow_origin: int = 0) -> None:
+                 n_flows: int | None = None, flow_of=None, flow_origin: int = 0, err=None) -> None:
     """Rewrite bytes [edit_off, edit_off+edit_len) of every packet with new_bytes[i*new_stride:] and patch
-    the big-endian checksum field at ck_off incrementally (RFC 1624); see pipck_update_fixed."""
+    the big-endian checksum field at ck_off incrementally (RFC 1624); see pipck_update_fixed_n.  A
+    flow_of entry >= n_flows (default: the tables' length) leaves its packet untouched and ORs
+    1 << PIPCK_ERANGE into err (optional device int32)."""
+    if pseudo_old is not None and pseudo_new is not None and pseudo_old.numel() != pseudo_new.numel():
+        raise ValueError("pseudo_old and pseudo_new must have the same number of flows")
     _check_span(arena, stride, cover_off + cover_len, n)
     if edit_len and new_bytes is not None and n and \
             (n - 1) * new_stride + edit_len > new_bytes.numel() * new_bytes.element_size():
         raise ValueError("new_bytes is too small for the batch")
-    call("pipck_update_fixed", _ptr(arena), stride, n, cover_off, cover_len, ck_off, edit_off, edit_len,
-         _ptr(new_bytes), new_stride, _ptr(pseudo_old), _ptr(pseudo_new), n_flows, _ptr(flow_of), flow_origin,
-         current_stream(arena.device))
+    call("pipck_update_fixed_n", _ptr(arena), stride, n, cover_off, cover_len, ck_off, edit_off, edit_len,
+         _ptr(new_bytes), new_stride, _ptr(pseudo_old), _ptr(pseudo_new), _n_flows(n_flows, pseudo_old, flow_of),
+         _ptr(flow_of), flow_origin, _ptr(err), current_stream(arena.device))
 
 
 def _check_span(arena, stride, length, n):

@@ -346,3 +346,186 @@ def test_flow_of_entry_past_the_table_is_an_error(layout, verify):
     assert (got[bad_at] == 0).all()
     keep = np.setdiff1d(np.arange(n), bad_at)
     assert np.array_equal(got[keep], good[keep])
+
+
+# ---------------------------------------------------------------------------
+# the fixed-stride flow index is bounded on the device too
+# ---------------------------------------------------------------------------
+# (stride, len, arena offset, tune, kernel): every fixed launch shape that reads
+# a flow_of entry, each asserted by name through pipck_last_launch
+FIXED_SHAPES = {
+    "coop_cfg2": (1488, 1480, 0, {}, "k_flat_coop<32"),
+    "coop_jumbo": (8992, 8980, 0, {}, "k_flat_coop<32"),
+    "flat_1k": (1024, 1000, 0, {}, "k_flat<32"),
+    "flat_alt": (1488, 1480, 0, {"alt_flat_schedule": True}, "k_flat<24"),
+    "flat_small": (256, 250, 0, {}, "k_flat_small<16"),
+    "flat_tiny": (40, 36, 0, {}, "k_flat_tiny<4"),
+    "small": (44, 40, 0, {}, "k_small<"),
+    "fixed": (1001, 999, 3, {}, "k_fixed<"),
+    "wave": (1488, 1480, 0, {"lanes_per_packet": 256}, "k_wave<"),
+}
+
+
+def _fixed_call(fn, arena, stride, length, n, pseudo, n_flows, flow_of, verify):
+    lib = _lib.load()
+    out = torch.full((n,), 0x5A, dtype=torch.uint8 if verify else torch.int16, device="cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    args = [_p(arena), C.c_uint64(stride), C.c_uint32(length), C.c_uint64(n), _p(pseudo), C.c_uint32(n_flows),
+            _p(flow_of), C.c_uint64(0), _p(out)]
+    rc = getattr(lib, fn)(*args, *([_p(err)] if fn.endswith("_n") else []), C.c_void_p(0))
+    torch.cuda.synchronize()
+    assert rc == 0, lib.pipck_last_error()
+    from tests.test_gpu_rx import _last_kernel
+
+    return out.cpu().numpy().view(np.uint8 if verify else np.uint16), int(err.item()), _last_kernel()
+
+
+@pytest.mark.parametrize("shape", list(FIXED_SHAPES))
+@pytest.mark.parametrize("verify", [False, True])
+def test_fixed_flow_of_entry_past_the_table_is_an_error(oracle, shape, verify):
+    """pipck_{checksum,verify}_fixed_n through ctypes, no Python guard: flow_of
+    entries >= n_flows planted at a block task's first and last packet and at the
+    batch's last packet (plus 0xFFFFFFFF and 2^30) give their packets 0 (verify 0)
+    and d_err = 1 << PIPCK_ERANGE, the pseudo table is never read there, and every
+    other packet equals the run with valid entries -- which equals the trusted
+    plain call and pip's pip_inet_checksum (oracle) -- under every fixed launch
+    shape, the kernel asserted by name."""
+    stride, length, off, knobs, kname = FIXED_SHAPES[shape]
+    n, n_flows, seed, proto = 64 * 13 + 29, 8, 901, 6
+    rng = np.random.default_rng(len(shape) * 7 + stride)
+    host = rng.integers(0, 256, off + n * stride + 64, dtype=np.uint8)
+    base = torch.from_numpy(host).to("cuda")
+    arena = base[off:]
+    _, pseudo = engine.gen_flows(4, n_flows, seed, proto)
+    flows = rng.integers(0, n_flows, n).astype(np.int32)
+    fn = "pipck_verify_fixed" if verify else "pipck_checksum_fixed"
+    engine.tune(**knobs)
+    try:
+        d_fl = torch.from_numpy(flows).to("cuda")
+        good, err0, k0 = _fixed_call(fn + "_n", arena, stride, length, n, pseudo, n_flows, d_fl, verify)
+        plain, _, _ = _fixed_call(fn, arena, stride, length, n, pseudo, n_flows, d_fl, verify)
+        # block tasks of 128 packets (k_flat_coop at 1,488 B), 24 (jumbo), wave tasks of 16-64:
+        # every such boundary below is a first or last packet of some task
+        bad_at = sorted({0, 23, 24, 63, 64, 127, 128, 255, 256, 383, 384, n - 2, n - 1})
+        fl2 = flows.copy()
+        fl2[bad_at] = [n_flows, 1 << 30, -1, n_flows + 1] * 3 + [n_flows]  # -1: 0xFFFFFFFF as u32
+        d_fl2 = torch.from_numpy(fl2).to("cuda")
+        got, err, k1 = _fixed_call(fn + "_n", arena, stride, length, n, pseudo, n_flows, d_fl2, verify)
+    finally:
+        engine.tune()
+    assert kname in k0 and kname in k1, (k0, k1)
+    assert err0 == 0 and np.array_equal(good, plain)
+    assert err == ERANGE_BIT
+    assert (got[bad_at] == 0).all()
+    keep = np.setdiff1d(np.arange(n), bad_at)
+    assert np.array_equal(got[keep], good[keep])
+    if verify:
+        return
+    for i in list(range(0, n, 97)) + [n - 3]:
+        pkt = host[off + i * stride:off + i * stride + length].tobytes()
+        s, d = oracle.flow4(seed, int(flows[i]))
+        assert good[i] == oracle.inet_checksum(pkt, proto, s, d), i
+
+
+def test_fixed_n_requires_n_flows():
+    """The bounded fixed forms refuse n_flows == 0 with a pseudo table (the plain
+    form with flow_of ignores n_flows, as before)."""
+    lib = _lib.load()
+    arena = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    _, pseudo = engine.gen_flows(4, 4, 1, 6)
+    fl = torch.zeros(2, dtype=torch.int32, device="cuda")
+    out = torch.zeros(2, dtype=torch.int16, device="cuda")
+    rc = lib.pipck_checksum_fixed_n(_p(arena), C.c_uint64(1488), C.c_uint32(1480), C.c_uint64(2), _p(pseudo),
+                                    C.c_uint32(0), _p(fl), C.c_uint64(0), _p(out), C.c_void_p(0), C.c_void_p(0))
+    assert rc == _lib.PIPCK_EINVAL
+    rc = lib.pipck_checksum_fixed(_p(arena), C.c_uint64(1488), C.c_uint32(1480), C.c_uint64(2), _p(pseudo),
+                                  C.c_uint32(0), _p(fl), C.c_uint64(0), _p(out), C.c_void_p(0))
+    torch.cuda.synchronize()
+    assert rc == 0
+
+
+def test_engine_flow_of_defaults_to_the_whole_table(oracle):
+    """an engine call with flow_of and no n_flows bounds the entries by
+    the whole pseudo table (pseudo.numel()), never by 1 -- fixed, packed and
+    byte-packed forms give every packet its flow's checksum."""
+    n, n_flows, seed, proto, stride, length = 300, 16, 77, 6, 1488, 1480
+    rng = np.random.default_rng(11)
+    host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    arena = torch.from_numpy(host).to("cuda")
+    _, pseudo = engine.gen_flows(4, n_flows, seed, proto)
+    flows = rng.integers(0, n_flows, n).astype(np.int32)
+    d_fl = torch.from_numpy(flows).to("cuda")
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    got = engine.checksum_fixed(arena, stride, length, n, pseudo, flow_of=d_fl, err=err).cpu().numpy().view(np.uint16)
+    for i in range(0, n, 13):
+        s, d = oracle.flow4(seed, int(flows[i]))
+        assert got[i] == oracle.inet_checksum(host[i * stride:i * stride + length].tobytes(), proto, s, d), i
+    w = CFG4
+    pa, lens, index, _ = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+    a = engine.checksum_packed_bytes(pa, lens, index, n, pseudo, flow_of=d_fl, err=err)
+    b = engine.checksum_packed_bytes(pa, lens, index, n, pseudo, n_flows, flow_of=d_fl, err=err)
+    pa16, lens16, index16, _ = engine.gen_packed(n, 0, w.seed, w.hdr)
+    c = engine.checksum_packed(pa16, lens16, index16, n, pseudo, flow_of=d_fl, err=err)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert torch.equal(a, b) and torch.equal(a, c)
+    assert int((a != 0).sum().item()) > n - 5
+
+
+def _update_case(n, stride, length, seed, proto, n_flows, rng):
+    host = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    host.reshape(n, stride)[:, 16:18] = 0  # th_sum is zero while pip sums the segment
+    arena = torch.from_numpy(host).to("cuda")
+    _, p_old = engine.gen_flows(4, n_flows, seed, proto)
+    _, p_new = engine.gen_flows(4, n_flows, seed ^ 0x5EED, proto)
+    flows = rng.integers(0, n_flows, n).astype(np.int32)
+    d_fl = torch.from_numpy(flows).to("cuda")
+    out = engine.checksum_fixed(arena, stride, length, n, p_old, n_flows, d_fl)
+    rows = arena.view(n, stride)
+    v = out.to(torch.int32) & 0xFFFF
+    rows[:, 16] = (v >> 8).to(torch.uint8)  # th_sum, htons() as pip's callers store it
+    rows[:, 17] = (v & 0xFF).to(torch.uint8)
+    return arena, p_old, p_new, flows
+
+
+def test_update_fixed_flow_of_entry_past_the_table_leaves_the_packet(oracle):
+    """pipck_update_fixed_n through ctypes: a packet whose flow_of entry is past the
+    tables keeps every byte (its edit is not applied, its field not patched) and
+    d_err = 1 << PIPCK_ERANGE; every other packet equals the untampered update,
+    which equals pip's full recomputation with the new addresses."""
+    n, stride, length, seed, proto, n_flows = 64 * 9 + 5, 1488, 1480, 515, 6, 8
+    rng = np.random.default_rng(21)
+    arena, p_old, p_new, flows = _update_case(n, stride, length, seed, proto, n_flows, rng)
+    before = arena.cpu().numpy().copy()
+    new = torch.from_numpy(rng.integers(0, 256, n * 8, dtype=np.uint8)).to("cuda")
+    lib = _lib.load()
+
+    def run(a, fl):
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        d_fl = torch.from_numpy(fl).to("cuda")
+        rc = lib.pipck_update_fixed_n(_p(a), C.c_uint64(stride), C.c_uint64(n), C.c_uint32(0), C.c_uint32(length),
+                                      C.c_uint32(16), C.c_uint32(0), C.c_uint32(8), _p(new), C.c_uint64(8),
+                                      _p(p_old), _p(p_new), C.c_uint32(n_flows), _p(d_fl), C.c_uint64(0), _p(err),
+                                      C.c_void_p(0))
+        torch.cuda.synchronize()
+        assert rc == 0, lib.pipck_last_error()
+        return a.cpu().numpy(), int(err.item())
+
+    good, err0 = run(arena.clone(), flows)
+    assert err0 == 0
+    bad_at = [0, 63, 64, 255, n - 1]
+    fl2 = flows.copy()
+    fl2[bad_at] = [n_flows, -1, 1 << 31, n_flows + 7, 100]
+    got, err = run(arena.clone(), fl2)
+    assert err == ERANGE_BIT
+    g2, b2, h2 = got.reshape(n, stride), good.reshape(n, stride), before.reshape(n, stride)
+    assert np.array_equal(g2[bad_at], h2[bad_at])  # refused packets: untouched, every byte
+    keep = np.setdiff1d(np.arange(n), bad_at)
+    assert np.array_equal(g2[keep], b2[keep])
+    # the untampered update equals pip's recomputation over the new bytes and addresses
+    for i in list(range(0, n, 41)) + [n - 2]:
+        pkt = bytearray(b2[i, :length].tobytes())
+        field = (pkt[16] << 8) | pkt[17]
+        pkt[16] = pkt[17] = 0
+        s, d = oracle.flow4(seed ^ 0x5EED, int(flows[i]))
+        assert field == oracle.inet_checksum(bytes(pkt), proto, s, d), i
