@@ -127,6 +127,18 @@ def kat_cases(rng: random.Random) -> list[dict]:
                      "mul": rng.randint(1, 255), "add": rng.randint(0, 255)} for _ in range(rng.randint(1, 5))]
             C.append({"fn": kind, "segs": segs, "proto": rng.randint(0, 255),
                       "src": rng.randbytes(w).hex(), "dst": rng.randbytes(w).hex()})
+    # chains whose pip_buf::total_len passes 65,535 (missing 2): pip adds
+    # the u32 total_len to the pseudo-header as hi + lo (pip_checksum.cpp:105-107,
+    # 139-141), so the hi term is non-zero here; every segment stays <= 65,535 B
+    for fam_fn, w in (("inet_chain", 4), ("inet6_chain", 16)):
+        for lens in ([40000, 40000], [30001, 30001, 30001], [65535, 1], [65535] * 4):
+            segs = [{"pattern": "affine", "len": L, "mul": rng.randint(1, 255), "add": rng.randint(0, 255)}
+                    for L in lens]
+            C.append({"fn": fam_fn, "segs": segs, "proto": rng.choice([6, 17]),
+                      "src": rng.randbytes(w).hex(), "dst": rng.randbytes(w).hex()})
+        # the largest sums pip's per-segment loop can carry: all-0xFF segments and addresses
+        C.append({"fn": fam_fn, "segs": [{"pattern": "const", "byte": 255, "len": 65535}] * 4, "proto": 255,
+                  "src": (b"\xff" * w).hex(), "dst": (b"\xff" * w).hex()})
     return C
 
 

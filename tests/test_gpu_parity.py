@@ -991,6 +991,89 @@ def test_chains_vs_oracle(oracle, fam):
         assert got[p] == fn(chain, proto, s, d), p
 
 
+def _chain_kats(kat, fn):
+    from tests.golden.make_golden import pattern_bytes
+
+    out = []
+    for c in kat:
+        if c["fn"] == fn:
+            segs = [pattern_bytes(x) for x in c["segs"]]
+            out.append((segs, c["proto"], bytes.fromhex(c["src"]), bytes.fromhex(c["dst"]), c["expect"]))
+    return out
+
+
+@pytest.mark.parametrize("fam", [4, 6])
+def test_chain_known_answers_through_the_batch_chain_abi(kat, fam):
+    """Every pip_inet{,6}_checksum_buf known answer (pip's compiled results, kat.json)
+    through pipck_checksum_chains_n, each chain its own packet with its own flow --
+    including the chains whose total_len passes 65,535 (2 x 40,000, 3 x 30,001 odd,
+    65,535 + 1, 4 x 65,535, all-0xFF 4 x 65,535), where pip's pseudo-header gets a
+    non-zero hi16(total_len) (pip/pip_checksum.cpp:105-107, 139-141).  Segments
+    sit at odd and even arena offsets."""
+    cases = _chain_kats(kat, "inet_chain" if fam == 4 else "inet6_chain")
+    assert sum(1 for c in cases if sum(len(x) for x in c[0]) > 65535) >= 5
+    rng = np.random.default_rng(fam * 7)
+    blob, offs, lens, seg_begin, flows = bytearray(), [], [], [0], bytearray()
+    for segs, proto, src, dst, _ in cases:
+        for sg in segs:
+            blob += bytes(int(rng.integers(0, 4)))  # odd / even starts
+            offs.append(len(blob))
+            lens.append(len(sg))
+            blob += sg
+        seg_begin.append(len(offs))
+        flows += src + dst + bytes([proto]) + bytes(3)  # pipck_flow4 / pipck_flow6 record
+    host = np.frombuffer(bytes(blob) + bytes(16), dtype=np.uint8)
+    _, arena = upload(host, 5)
+    pseudo = engine.prepare_flows(fam, engine.flows_to_device(fam, bytes(flows)), len(cases))
+    segs_d = engine.make_desc(np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32), np.zeros(len(offs)))
+    pkt_flow = torch.arange(len(cases), dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    got = u16(engine.checksum_chains(arena, segs_d, torch.tensor(seg_begin, dtype=torch.int64, device=DEV), pkt_flow,
+                                     pseudo, err=err))
+    assert int(err.item()) == 0
+    want = np.array([c[4] for c in cases], dtype=np.uint16)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(i), [len(x) for x in cases[i][0]], int(want[i]), int(got[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("in_place", [True, False])
+def test_chain_known_answers_through_the_tx_queue(kat, in_place):
+    """The same known answers (v4 and v6 chains, the > 65,535-B totals among them)
+    through the deferred TX queue (pipck_txq_add4 / add6 + flush): each field gets
+    htons() of pip's own result, in place and with the copy path."""
+    lib = _lib.load()
+    ctx, q = C.c_void_p(), C.c_void_p()
+    _lib.check("pipck_ctx_create", lib.pipck_ctx_create(-1, C.byref(ctx)))
+    _lib.check("pipck_txq_create", lib.pipck_txq_create(ctx, C.byref(q)))
+    if not in_place:
+        _lib.check("pipck_txq_inplace_max", lib.pipck_txq_inplace_max(q, 0))
+    cases = [(4, c) for c in _chain_kats(kat, "inet_chain")] + [(6, c) for c in _chain_kats(kat, "inet6_chain")]
+    fields = (C.c_uint8 * (2 * len(cases)))()
+    keep = []
+    try:
+        for i, (fam, (segs, proto, src, dst, _)) in enumerate(cases):
+            arr = (_lib.HSeg * max(len(segs), 1))()
+            for j, sg in enumerate(segs):
+                b = C.create_string_buffer(sg, max(len(sg), 1))
+                keep.append(b)
+                arr[j].ptr = C.cast(b, C.c_void_p)
+                arr[j].len = len(sg)
+            field = C.c_void_p(C.addressof(fields) + 2 * i)
+            if fam == 4:
+                _lib.check("add4", lib.pipck_txq_add4(q, arr, len(segs), proto, int.from_bytes(src, "little"),
+                                                      int.from_bytes(dst, "little"), field))
+            else:
+                _lib.check("add6", lib.pipck_txq_add6(q, arr, len(segs), proto, src, dst, field))
+        _lib.check("pipck_txq_flush", lib.pipck_txq_flush(q))
+        got = np.frombuffer(bytes(fields), dtype=">u2")
+        want = np.array([c[4] for _, c in cases], dtype=np.uint16)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(int(i), [len(x) for x in cases[i][1][0]], int(want[i]), int(got[i])) for i in bad[:5]]
+    finally:
+        lib.pipck_txq_destroy(q)
+        lib.pipck_ctx_destroy(ctx)
+
+
 # ----------------------------------------------------------------------------
 # 5. RX verification kernel
 # ----------------------------------------------------------------------------
