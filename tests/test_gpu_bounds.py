@@ -356,7 +356,7 @@ def test_flow_of_entry_past_the_table_is_an_error(layout, verify):
 FIXED_SHAPES = {
     "coop_cfg2": (1488, 1480, 0, {}, "k_flat_coop<32"),
     "coop_jumbo": (8992, 8980, 0, {}, "k_flat_coop<32"),
-    "flat_1k": (1024, 1000, 0, {}, "k_flat<32"),
+    "flat_1k": (1024, 1000, 0, {}, "k_flat<24"),
     "flat_alt": (1488, 1480, 0, {"alt_flat_schedule": True}, "k_flat<24"),
     "flat_small": (256, 250, 0, {}, "k_flat_small<16"),
     "flat_tiny": (40, 36, 0, {}, "k_flat_tiny<4"),
@@ -515,7 +515,7 @@ def test_update_fixed_flow_of_entry_past_the_table_leaves_the_packet(oracle):
     assert err0 == 0
     bad_at = [0, 63, 64, 255, n - 1]
     fl2 = flows.copy()
-    fl2[bad_at] = [n_flows, -1, 1 << 31, n_flows + 7, 100]
+    fl2[bad_at] = [n_flows, -1, -(1 << 31), n_flows + 7, 100]  # -(1 << 31): 0x80000000 as u32
     got, err = run(arena.clone(), fl2)
     assert err == ERANGE_BIT
     g2, b2, h2 = got.reshape(n, stride), good.reshape(n, stride), before.reshape(n, stride)

@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 420 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
+  timeout -k 10 420 python3 -u -m pytest tests -m gpu ${PYTEST_X:--x} -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} \
     > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -2 gpurun_out/pytest_gpu.log
 fi
