@@ -110,14 +110,18 @@ def last_kernel() -> str:
 
 
 class HipEvents:
-    """n timing events of the HIP runtime torch loaded (the library libpipck
-    launches through), recorded on one stream by raw hipEventRecord."""
+    """n timing events of the HIP runtime already mapped into the process (the
+    one libpipck launches through, engine.hip_runtime), recorded on one stream
+    by raw hipEventRecord."""
 
     def __init__(self, n: int, stream: int | None):
         import ctypes as C
 
         self._C = C
-        self.hip = C.CDLL("libamdhip64.so")
+        # RTLD_NOLOAD: a handle on the mapped instance, never a fresh load
+        from pip_amd import engine
+
+        self.hip = engine.hip_runtime()
         self.hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
         self.hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
         self.hip.hipEventDestroy.argtypes = [C.c_void_p]
@@ -479,6 +483,34 @@ def host_e2e_packed(w, dev, n, flows, want):
             "results_match": bool(np.array_equal(out, want))}
 
 
+def mem_available() -> int:
+    """MemAvailable of /proc/meminfo in bytes (0 if unreadable)."""
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 0
+
+
+def host_bytes_per_packet(w) -> int:
+    """Host memory the CPU legs hold per sampled packet: the packet bytes (a fixed
+    slot, or cfg4's Zipf mean rounded up generously), the pip_buf chain copy the
+    chain leg builds, results and per-packet metadata."""
+    per = w.stride if not w.ragged else 1024
+    return 2 * per + 64
+
+
+def sample_that_fits(n: int, per_packet: int) -> int:
+    """n, or the largest sample whose host footprint fits a quarter of MemAvailable."""
+    avail = mem_available()
+    if not avail or n * per_packet <= avail // 4:
+        return n
+    return max(1 << 12, int(avail // 4 // per_packet))
+
+
 def cpu_legs(args, w, gpu_out, count, first, dev=None):
     """pip's own checksum on the host cores over a bounded sample of the same
     packets (checked bit-exact against the GPU results), plus the PCIe-inclusive
@@ -498,10 +530,15 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
 
     # the sample BASELINE.md ("Which inputs") prescribes: the full batch for cfg1-cfg4,
     # the first 1M packets for cfg5 (64M x 8,980 B cannot be host-resident) -- up to
-    # ~9 GB of host memory (cfg3, cfg5); --cpu-sample overrides it
+    # ~9 GB of host memory (cfg3, cfg5); --cpu-sample overrides it.  A host with too
+    # little free memory for that gets the largest sample that fits in a quarter of
+    # what is available, and the line's "sample" says so.
     plan = f"BASELINE.md plan: {'first 1M packets of the per-GPU shard' if w.cfg == 5 else 'the full batch'}"
+    n_plan = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)
+    n = sample_that_fits(n_plan, host_bytes_per_packet(w))
+    if n < n_plan:
+        plan += f"; FELL BACK to {n} of {n_plan} packets: {mem_available() >> 20} MiB of host memory available"
     if w.ragged:
-        n = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)
         arena, offs, lens = orc.gen_ragged_batch(w.seed, first, n, w.hdr, threads)
         l4 = int(lens.astype(np.int64).sum())
 
@@ -518,7 +555,7 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
         st = l4 / (time.perf_counter() - t0) / 2**30
         cpu = {"value": round(l4 * reps / el / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
                "sample": f"first {n} packets of the same Zipf workload ({l4 / 2**30:.2f} GiB of L4 bytes; "
-                         f"{plan if not args.cpu_sample else '--cpu-sample'}), "
+                         f"{plan if not args.cpu_sample or n < n_plan else '--cpu-sample'}), "
                          f"pip_inet_checksum per packet, {reps} timed passes on {threads} threads; "
                          f"1 thread: {st:.3f} GiB/s",
                "single_core_gib_per_s": round(st, 3), "gpu_results_match": verified,
@@ -527,7 +564,6 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
             {"value": None, "note": "host end-to-end: rank 0 of a one-rank run only"}
         return cpu, e2e
 
-    n = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)
     lib = _lib.load()
     pin = lib.pipck_host_alloc(n * w.stride)
     if not pin:
@@ -570,7 +606,7 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
     what = "pip_ip_checksum" if not w.family else f"pip_inet{'6' if w.family == 6 else ''}_checksum"
     cpu = {"value": round(mt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
            "sample": f"first {n} packets of the same workload ({n * w.length / 2**30:.3f} GiB; "
-                     f"{plan if not args.cpu_sample else '--cpu-sample'}), {what} per packet, "
+                     f"{plan if not args.cpu_sample or n < n_plan else '--cpu-sample'}), {what} per packet, "
                      f"{reps} timed passes on {threads} threads; 1 thread: {st:.3f} GiB/s",
            "single_core_gib_per_s": round(st, 3),
            "mpkt_per_s": round(n * reps / el / 1e6, 2), "single_core_mpkt_per_s": round(n * reps1 / el1 / 1e6, 2),

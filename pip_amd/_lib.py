@@ -117,6 +117,7 @@ SIGNATURES = {
 INTERNAL_SIGNATURES = {
     "pipck_tune": (None, [_u32, _u32, _u32, _u32]),
     "pipck_tune_probes": (None, [_u32]),
+    "pipck_tune_ring": (None, [_u32]),
     "pipck_trace_tasks": (_i32, [_p, _u64]),
     "pipck_tune_xcd_weights": (_i32, [_p, _u32]),
     "pipck_last_launch": (_i32, [C.c_char_p, _sz]),

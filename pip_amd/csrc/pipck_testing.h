@@ -57,11 +57,9 @@ extern "C" {
  * Bit 28 = the other fixed-stride schedule (and for pipck_rx_verify_ring the
  * row stream k_ring_rx instead of the default k_ring; lanes_per_packet = 256
  * there selects k_ring_slots, loads_per_lane 8 / 24 k_ring's loads in flight,
- * and bits 29 / 27 make k_ring's row stream never / always deal its items
- * round-robin to the block's waves -- bit 27 is also the top bit of the small
- * kernel's depth field below, so set it for ring measurements only; the blocks
- * argument 8 / 16 / 32 makes that interleaved stream cover so many slots at a
- * time): k_flat (one task per wave)
+ * the blocks argument 8 / 16 / 32 makes its interleaved row stream cover so
+ * many slots at a time; its other switches are pipck_tune_ring's, below):
+ * k_flat (one task per wave)
  * instead of the block-cooperative k_flat_coop, the default for 16-B-multiple
  * strides from 1 KiB to 64 KiB except exactly 1 and 2 KiB (there the reverse);
  * for k_flat_coop, bits 8..15 are rows per wave
@@ -87,6 +85,14 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
  * untouched (the "results inside the headers" layout).
  * 0 switches every probe off. */
 void pipck_tune_probes(uint32_t probes);
+
+/* The ring verifier's schedule (pipck_rx_verify_ring; process-wide, internal,
+ * every setting gives the same verdicts): 0 = automatic -- k_ring, and for slot
+ * strides from 4 KiB its dense slot groups verified by k_ring_deep on a second
+ * stream at the same time.  Bit 0 = k_ring's row stream never deals items
+ * round-robin to the block's waves, bit 1 = always; bit 2 = no dense-group
+ * split (k_ring alone, the round-5 default); bit 3 = the split at every stride. */
+void pipck_tune_ring(uint32_t mode);
 
 /* XCD-weighted static deal for k_flat (ring 24, checksum; measurement arm,
  * VERDICT r03 item 7): the grid is cut into periods of 8 x period blocks and

@@ -42,15 +42,42 @@ def require_gpu() -> None:
     load()
 
 
+_hip = None
+
+
+def hip_runtime() -> C.CDLL:
+    """A handle on THE HIP runtime mapped into this process -- the one libpipck.so
+    links and launches through, and whose streams torch hands us.  Opening
+    "libamdhip64.so" by its bare name could load a second runtime instance (another
+    soname or path); events or queries made through it would not see this
+    runtime's streams.  So the library is found in /proc/self/maps after
+    libpipck.so is loaded and opened with RTLD_NOLOAD (never a fresh load); more
+    than one mapped runtime is an error."""
+    global _hip
+    if _hip is None:
+        import os
+
+        load()
+        paths = set()
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and os.path.basename(parts[5]).startswith("libamdhip64.so"):
+                    paths.add(os.path.realpath(parts[5]))
+        if len(paths) != 1:
+            raise RuntimeError(f"expected exactly one HIP runtime mapped in this process, found {sorted(paths)}")
+        _hip = C.CDLL(paths.pop(), mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+    return _hip
+
+
 def pci_bus_id(device: int) -> str:
     """PCI bus id of a HIP device ("0000:05:00.0"), from hipDeviceGetPCIBusId: names the physical
     GPU a rank ran on (bench.py's per_rank_device)."""
     buf = C.create_string_buffer(64)
     try:
-        hip = C.CDLL("libamdhip64.so")
-        if hip.hipDeviceGetPCIBusId(buf, C.c_int(len(buf)), C.c_int(device)) == 0:
+        if hip_runtime().hipDeviceGetPCIBusId(buf, C.c_int(len(buf)), C.c_int(device)) == 0:
             return buf.value.decode()
-    except OSError:
+    except (OSError, RuntimeError):
         pass
     p = _torch().cuda.get_device_properties(device)
     return f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:" \
@@ -552,14 +579,16 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          end_no_store: bool = False, alt_flat_schedule: bool = False,
          plain_result_stores: bool = False, wave_stores: bool = False, free_run: bool = False,
          packed_no_align: bool = False, hdr_in_place: bool = False, ring_own_slots: bool = False,
-         ring_all_coop: bool = False) -> None:
+         ring_all_coop: bool = False, ring_deep: bool | None = None) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
     except the measurement-only probes loads_only (bit 21), no_task_end (22), end_no_store (23) and
     hdr_in_place (pipck_tune_probes bit 0, not a tune flag: k_hdr stores the results into the headers'
     ip_sum and leaves the result array untouched).  alt_flat_schedule (bit 28) never changes results.
     ring_own_slots / ring_all_coop: k_ring's row stream never / always deals items round-robin to the
-    block's waves (bits 29 / 27, read by pipck_rx_verify_ring only)."""
+    block's waves; ring_deep: None = automatic (jumbo slots split their dense groups off to
+    k_ring_deep), False = k_ring alone, True = the split at every stride -- all pipck_tune_ring's own
+    word, apart from the flags above (they once shared bits 27 / 29)."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
@@ -568,8 +597,10 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (0 if flat_tiny else 1 << 17) | (1 << 18 if force_flat_tiny else 0) | (small_k_log << 24)
              | (1 << 19 if packed_marks_only else 0) | (1 << 20 if trace else 0) | (1 << 21 if loads_only else 0) | (1 << 22 if no_task_end else 0)
              | (1 << 23 if end_no_store else 0) | (1 << 28 if alt_flat_schedule else 0)
-             | (1 << 29 if (plain_result_stores or ring_own_slots) else 0) | (1 << 27 if ring_all_coop else 0)
+             | (1 << 29 if plain_result_stores else 0)
              | (1 << 30 if (wave_stores or packed_no_align) else 0)
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
     load().pipck_tune_probes(1 if hdr_in_place else 0)
+    load().pipck_tune_ring((1 if ring_own_slots else 0) | (2 if ring_all_coop else 0)
+                           | {None: 0, False: 4, True: 8}[ring_deep])

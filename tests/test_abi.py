@@ -45,7 +45,8 @@ def test_libpipck_exports_every_declared_function():
 def test_internal_tuning_hook_is_outside_the_public_header():
     internal = header_functions(ROOT / "pip_amd" / "csrc" / "pipck_testing.h")
     assert internal == sorted(_lib.INTERNAL_SIGNATURES) == ["pipck_last_launch", "pipck_trace_tasks", "pipck_tune",
-                                                            "pipck_tune_probes", "pipck_tune_xcd_weights"]
+                                                            "pipck_tune_probes", "pipck_tune_ring",
+                                                            "pipck_tune_xcd_weights"]
     for f in internal:
         assert f in dynsyms(_lib.LIBPIPCK)  # still exported, for tests/ and tools/
 

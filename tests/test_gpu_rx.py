@@ -442,8 +442,10 @@ def _ring(frames, stride):
 # pipck_rx_verify_ring's three schedules (pipck_rxdev.hip): the default slot
 # groups (k_ring), the row stream (k_ring_rx, tune flag bit 28) and slot by slot
 # (k_ring_slots, the wave-per-packet arm)
+# (plus, from 4 KiB slots, k_ring_deep on a second stream for the dense slot
+# groups; "nodeep" = k_ring alone, "deep" = that split at every stride)
 RING_KERNELS = {"groups": "k_ring<8, 12>", "own": "k_ring<8, 12>", "coop": "k_ring<8, 12>", "rows": "k_ring_rx",
-                "slots": "k_ring_slots"}
+                "slots": "k_ring_slots", "deep": "k_ring<8, 12>", "nodeep": "k_ring<8, 12>"}
 
 
 def _ring_schedule(name):
@@ -457,6 +459,10 @@ def _ring_schedule(name):
         engine.tune(ring_own_slots=True)
     elif name == "coop":  # k_ring's row stream: items dealt round-robin to the block's waves
         engine.tune(ring_all_coop=True)
+    elif name == "deep":  # dense slot groups to k_ring_deep at every stride
+        engine.tune(ring_deep=True)
+    elif name == "nodeep":  # k_ring alone (the round-5 default)
+        engine.tune(ring_deep=False)
     else:
         engine.tune()
 
@@ -464,7 +470,8 @@ def _ring_schedule(name):
 def _ring_frames(oracle, rng, stride, fill, count):
     """count oracle-checksummed IPv4/IPv6 TCP/UDP/ICMP frames that fit the slot,
     every third damaged, some with link padding.  fill "mixed": L4 lengths up to
-    the slot; "short": frames in runs of 16 whose longest is <= 128 / 256 / 512
+    the slot; "dense": within ~200 B of filling the slot (k_ring_deep's groups),
+    with a run of short frames every 512; "short": frames in runs of 16 whose longest is <= 128 / 256 / 512
     bytes or up to the slot, so k_ring's waves take every schedule (S = 8, 16, 32
     lanes per slot, and the row stream)."""
     frames = []
@@ -472,8 +479,10 @@ def _ring_frames(oracle, rng, stride, fill, count):
         fam = rng.choice([4, 6])
         proto = rng.choice([6, 17, 1]) if fam == 4 else rng.choice([6, 17, 58])
         hl = 20 if fam == 4 else 40
-        cap = stride if fill == "mixed" else (128, 256, 512, stride)[(k // 16) % 4]
-        l4len = rng.randint(20, min(9000, cap - hl - 7))
+        cap = stride if fill != "short" else (128, 256, 512, stride)[(k // 16) % 4]
+        top = min(9000, cap - hl - 7)
+        lo = max(20, top - 200) if fill == "dense" and (k // 64) % 8 != 5 else 20
+        l4len = rng.randint(lo, top)
         p = bytearray(_rx_packet(oracle, rng, fam, proto, l4len, k + 1))
         if k % 3 == 1:
             p[rng.randrange(len(p))] ^= 0x04
@@ -491,8 +500,8 @@ def _host_bits(frames):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fill", ["mixed", "short"])
-@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots"])
+@pytest.mark.parametrize("fill", ["mixed", "short", "dense"])
+@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots", "deep", "nodeep"])
 @pytest.mark.parametrize("stride", [1024, 2048, 9216])
 def test_rx_verify_ring_equals_host_path(oracle, stride, schedule, fill):
     """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused
