@@ -36,8 +36,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <memory>
-#include <vector>
 
 namespace pipck {
 
@@ -68,24 +66,18 @@ namespace pipck {
 constexpr int kRingU = 24;
 
 __host__ __device__ constexpr uint32_t ring_pitch(uint32_t k) { return k | 1u; }
-// LDS of one row-stream task of K slots: part[64][pitch] | len[K] | hdr[6][K] (u32x4)
-__host__ __device__ constexpr uint32_t ring_task_lds(uint32_t k) {
-    return 4u * (64u * ring_pitch(k) + ((k + 3u) & ~3u)) + 16u * 6u * k;
-}
 
-// One block task of the row stream: slots [p0, p0 + min(K, n - p0)), judged
-// into ok[]; s_ring holds ring_task_lds(K) bytes.  Ends with every thread done
-// with the LDS it read (the caller may start another task after a barrier).
-template <int U>
-__device__ __forceinline__ void ring_rx_task(uint32_t* s_ring, const uint8_t* __restrict__ arena, uint32_t cpp,
-                                             const uint16_t* __restrict__ lens, uint64_t n, uint64_t p0, uint32_t K,
-                                             uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_ring_rx(
+    const uint8_t* __restrict__ arena, uint32_t cpp, const uint16_t* __restrict__ lens, uint64_t n, uint32_t K,
+    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
+    extern __shared__ uint32_t s_ring[];  // part[64][pitch] | len[K] | hdr[6][K] (u32x4), launch_ring_rx sizes it
     const uint32_t pitch = ring_pitch(K);
     uint32_t* s_part = s_ring;
     uint32_t* s_len = s_part + 64u * pitch;
     u32x4* hdr = reinterpret_cast<u32x4*>(s_len + ((K + 3u) & ~3u));
     const int lane = threadIdx.x & 63;
     const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t p0 = (uint64_t)blockIdx.x * K;
     const uint32_t np = (uint32_t)min<uint64_t>((uint64_t)K, n - p0);
     const uint32_t rows = (np * cpp + 63u) >> 6;
     for (uint32_t i = threadIdx.x; i < 64u * pitch; i += 256) s_part[i] = 0;
@@ -125,15 +117,15 @@ __device__ __forceinline__ void ring_rx_task(uint32_t* s_ring, const uint8_t* __
         // turned every wait of the ring into vmcnt(0): the load always issues)
         return buf_load<true>(tb, 16u * k < L ? ((w + 4u * j) * 64u + (uint32_t)lane) * 16u : 0xFFFFFFF0u);
     };
-    u32x4 v[U];
+    u32x4 v[kRingU];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
+    for (int u = 0; u < kRingU; u++) {
         v[u] = load((uint32_t)u);
         step(lpkt, lk0);
     }
-    for (uint32_t j0 = 0; j0 < my_rows; j0 += U) {
+    for (uint32_t j0 = 0; j0 < my_rows; j0 += kRingU) {
 #pragma unroll
-        for (int u = 0; u < U; u++) {
+        for (int u = 0; u < kRingU; u++) {
             const uint32_t j = j0 + u;
             if (j < my_rows) {  // wave-uniform
                 uint32_t k = k0 + (uint32_t)lane, pk = pkt;
@@ -152,7 +144,7 @@ __device__ __forceinline__ void ring_rx_task(uint32_t* s_ring, const uint8_t* __
                 }
                 step(pkt, k0);
             }
-            v[u] = load(j + U);  // past the task: the resource's range check reads nothing
+            v[u] = load(j + kRingU);  // past the task: the resource's range check reads nothing
             step(lpkt, lk0);
         }
     }
@@ -175,13 +167,6 @@ __device__ __forceinline__ void ring_rx_task(uint32_t* s_ring, const uint8_t* __
         if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
         store_result8(buf_rsrc(ok + p0, np), i, bad ? 0u : rx_from_window(pkp, L, F, hw));
     }
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_ring_rx(
-    const uint8_t* __restrict__ arena, uint32_t cpp, const uint16_t* __restrict__ lens, uint64_t n, uint32_t K,
-    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
-    extern __shared__ uint32_t s_ring[];  // ring_task_lds(K) bytes, launch_ring_rx sizes it
-    ring_rx_task<kRingU>(s_ring, arena, cpp, lens, n, (uint64_t)blockIdx.x * K, K, ok, err);
 }
 
 // ---- the same ring, slot by slot (sparse rings: short frames in large slots) --
@@ -280,24 +265,12 @@ __global__ __launch_bounds__(256) void k_ring_slots(const uint8_t* __restrict__ 
 // rx_from_window, so one wave's parse is spread over 64 slots.
 constexpr uint32_t kRingB = 64;        // slots per block
 constexpr uint32_t kRingCoopRows = 2;  // mean rows per slot from which the waves interleave
-// pipck_tune_ring (pipck_testing.h): the ring verifier's schedule switches, a
-// word of their own (VERDICT/ADVICE r05: they once shared pipck_tune's flag bits)
-constexpr uint32_t kRingOwnSlots = 1u;  // k_ring's row stream: never interleave
-constexpr uint32_t kRingAllCoop = 2u;   // k_ring's row stream: always interleave
-constexpr uint32_t kRingNoDeep = 4u;    // no dense-group split: k_ring alone (the round-5 default)
-constexpr uint32_t kRingDeepAll = 8u;   // the dense-group split at every stride (tests; default from 4 KiB)
+// pipck_tune_ring (pipck_testing.h): k_ring's schedule switches, a word of their
+// own (they once shared pipck_tune's flag bits 27 / 29 with the
+// small kernel's depth and the result-store policy)
+constexpr uint32_t kRingOwnSlots = 1u;  // the row stream never interleaves its waves
+constexpr uint32_t kRingAllCoop = 2u;   // the row stream always interleaves them
 std::atomic<uint32_t> g_ring_mode{0};
-
-// Dense slot groups (the deep path).  A group of 64 slots (a k_ring block) is
-// dense when the 1 KiB rows holding frame bytes (T, from the 64 lengths) are at
-// least 3/4 of the rows of its slots -- full jumbo slots.  Both kernels of the
-// split evaluate exactly this on the same lengths, so they partition the groups
-// without exchanging anything: k_ring returns from a dense group before reading
-// a frame byte, and k_ring_deep verifies the dense groups alone.
-constexpr uint32_t kDeepMinStride = 4096;  // jumbo slots: below, k_ring runs every group itself
-__device__ __forceinline__ bool ring_dense(uint32_t T, uint32_t nb, uint32_t stride) {
-    return 4u * T >= 3u * nb * ((stride + 1023u) >> 10);
-}
 
 struct RingLds {
     u32x4 hdr[6][kRingB];  // chunk k of slot g's header window
@@ -415,9 +388,6 @@ __device__ __forceinline__ void ring_rows(RingLds& t, buf_t rb, uint32_t stride,
     if (cur != 0xFFFFFFFFu) flush(cur, acc);
 }
 
-// kflags: the pipck_tune_ring word, plus kRingDefer when k_ring_deep runs beside
-// this launch (the dense groups are then left to it)
-constexpr uint32_t kRingDefer = 1u << 16;
 template <int U, int UD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
                                               const uint16_t* __restrict__ lens, uint64_t n, uint32_t G,
@@ -437,10 +407,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ri
     const uint32_t Lc = bad ? 0u : L;  // the bytes this slot reads
     const uint32_t nch = (Lc + 15u) >> 4;
     const uint32_t cmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(nch), 63);
-    const uint32_t R = (nch + 63u) >> 6;  // 1 KiB rows holding frame bytes
-    // a dense group belongs to k_ring_deep (block-uniform: every wave read the
-    // same 64 lengths); nothing of it is read or written here
-    if ((kflags & kRingDefer) && ring_dense(wave_total(R), nb, stride)) return;
     if (w == 0) t.sum[lane] = 0;  // flushes add
     __syncthreads();
     const buf_t rb = buf_rsrc(arena + b0 * stride, nb * stride);  // the block's slots
@@ -452,6 +418,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ri
         else
             ring_short<32, 8>(t, rb, stride, nb, Lc, w, 4u, lane);
     } else {
+        const uint32_t R = (nch + 63u) >> 6;
         const uint32_t incl = wave_incl_scan(R);
         const uint32_t excl = incl - R;
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // the block's items
@@ -487,92 +454,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ri
     store_result8(buf_rsrc(ok + b0, nb), (uint32_t)lane, r);
 }
 
-// ---- the dense groups: a deep row stream at low occupancy (k_ring_deep) -----
-// k_ring keeps 8 waves per SIMD with shallow rings, which the sparse and
-// short-frame rings need (their bound is one scattered frame or line per slot);
-// on full jumbo slots that many concurrent windows run 2-3 % below the row
-// stream (k_ring_rx: ring 24, 3 waves per SIMD).  So jumbo
-// rings split: k_ring skips its dense groups, and this persistent kernel, on a
-// second stream at the same time, takes them -- 2 blocks per CU, a ring of U
-// rows per wave, each group as KS-slot row-stream tasks (ring_rx_task, the
-// k_ring_rx body).  Block b owns groups b, b + grid, b + 2 grid, ...: it reads
-// 64 of its groups' lengths at once (16 groups per wave, the loads issued
-// together), marks the dense ones, and streams them in order, so the blocks in
-// flight cover one contiguous window of the ring.  No list, no counter: both
-// kernels decide with ring_dense on the same lengths.
-template <int U>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_ring_deep(
-    const uint8_t* __restrict__ arena, uint32_t stride, const uint16_t* __restrict__ lens, uint64_t n, uint32_t KS,
-    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
-    extern __shared__ uint32_t s_ring[];  // ring_task_lds(KS) bytes, launch_ring_rx sizes it
-    __shared__ uint32_t s_dense[64];
-    const int lane = threadIdx.x & 63;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint64_t groups = (n + kRingB - 1) / kRingB;
-    const uint64_t G = gridDim.x;
-    for (uint64_t c0 = blockIdx.x; c0 < groups; c0 += 64u * G) {
-        // classify: wave w takes this batch's groups 16 w .. 16 w + 15
-        uint32_t L[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const uint64_t g = c0 + (uint64_t)(16u * w + k) * G;
-            const uint64_t slot = g * kRingB + (uint64_t)lane;
-            L[k] = g < groups && slot < n ? (uint32_t)lens[slot] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const uint64_t g = c0 + (uint64_t)(16u * w + k) * G;
-            const uint32_t Lc = L[k] > stride ? 0u : L[k];  // as k_ring: a refused slot reads nothing
-            const uint32_t T = wave_total((Lc + 1023u) >> 10);
-            const uint32_t nb = g < groups ? (uint32_t)min<uint64_t>(kRingB, n - g * kRingB) : 0u;
-            if (lane == 0) s_dense[16u * w + k] = nb && ring_dense(T, nb, stride) ? 1u : 0u;
-        }
-        __syncthreads();
-        for (uint32_t j = 0; j < 64; j++) {
-            if (!s_dense[j]) continue;  // block-uniform
-            const uint64_t g = c0 + (uint64_t)j * G;
-            for (uint32_t u = 0; u < kRingB; u += KS) {
-                const uint64_t p0 = g * kRingB + u;
-                if (p0 >= n) break;
-                ring_rx_task<U>(s_ring, arena, stride / 16u, lens, n, p0, KS, ok, err);
-                __syncthreads();  // the task's end has read its LDS: the next task may clear it
-            }
-        }
-        __syncthreads();  // s_dense is rewritten by the next batch
-    }
-}
-
-// A second stream per thread and device for k_ring_deep, and the events that
-// fork it from the caller's stream and join it back.
-struct RingAux {
-    int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    ~RingAux() {
-        if (s) (void)hipStreamDestroy(s);
-        if (fork) (void)hipEventDestroy(fork);
-        if (join) (void)hipEventDestroy(join);
-    }
-};
-static int ring_aux(RingAux** out) {
-    thread_local std::vector<std::unique_ptr<RingAux>> aux;
-    int dev = 0;
-    PIPCK_HIP(hipGetDevice(&dev));
-    for (auto& a : aux)
-        if (a->dev == dev) {
-            *out = a.get();
-            return PIPCK_OK;
-        }
-    auto a = std::make_unique<RingAux>();
-    a->dev = dev;
-    PIPCK_HIP(hipStreamCreateWithFlags(&a->s, hipStreamNonBlocking));
-    PIPCK_HIP(hipEventCreateWithFlags(&a->fork, hipEventDisableTiming));
-    PIPCK_HIP(hipEventCreateWithFlags(&a->join, hipEventDisableTiming));
-    *out = a.get();
-    aux.push_back(std::move(a));
-    return PIPCK_OK;
-}
-
 int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
                    uint32_t* d_err, hipStream_t s) {
     if (n == 0) return PIPCK_OK;
@@ -586,6 +467,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         return PIPCK_EINVAL;
     }
     const uint32_t cpp = (uint32_t)(stride / 16);
+    const uint32_t flags = g_ring_mode.load();
     if (wave_arm()) {  // measurement arm: slot by slot, a wave per slot
         const uint64_t blocks = (n + 4u * kSlotG - 1) / (4u * kSlotG);
         if (blocks > 0x7FFFFFFFull) {
@@ -608,7 +490,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
             set_error("pipck_rx_verify_ring: too many slots for one launch");
             return PIPCK_ERANGE;
         }
-        const size_t lds = ring_task_lds(K);
+        const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
         PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
                      d_ok, d_err);
         PIPCK_LAUNCHED("k_ring_rx");
@@ -633,30 +515,6 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     }
     const uint8_t* a = (const uint8_t*)d_arena;
     const uint32_t st = (uint32_t)stride;
-    // jumbo slots: the dense groups go to k_ring_deep on a second stream, forked
-    // from and joined back into the caller's (both kernels run at once: the deep
-    // one holds 2 blocks per CU, k_ring the rest)
-    const uint32_t mode = g_ring_mode.load();
-    const bool deep = !(mode & kRingNoDeep) && ((mode & kRingDeepAll) || stride >= kDeepMinStride);
-    uint32_t flags = mode & (kRingOwnSlots | kRingAllCoop);
-    RingAux* aux = nullptr;
-    if (deep) {
-        int rc = ring_aux(&aux);
-        if (rc) return rc;
-        // KS slots per row-stream task: ~4 waves x 64 rows, a power of two dividing 64
-        uint32_t KS = 64;
-        while (KS > 8 && (uint64_t)KS * stride > 256u * 1024u) KS >>= 1;
-        const uint32_t dgrid = (uint32_t)std::min<uint64_t>(blocks, (uint64_t)device_cus() * 2u);
-        PIPCK_HIP(hipEventRecord(aux->fork, s));
-        PIPCK_HIP(hipStreamWaitEvent(aux->s, aux->fork, 0));
-        hipLaunchKernelGGL((k_ring_deep<32>), dim3(dgrid), dim3(256), ring_task_lds(KS), aux->s, a, st, d_lens, n, KS,
-                           d_ok, d_err);
-        {
-            const hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return hip_fail(e, "k_ring_deep");
-        }
-        flags |= kRingDefer;
-    }
     // loads in flight per wave: U in the short and own-slot streams, UD in the
     // interleaved one (loads_per_lane 16 / 24: both; 17 / 25: UD only)
 #define PIPCK_RING(UU, UUD)                                                                                     \
@@ -672,17 +530,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         default: PIPCK_RING(8, 12); break;
     }
 #undef PIPCK_RING
-    {
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-            if (aux) (void)hipStreamSynchronize(aux->s);  // the deep half never outlives a failed call
-            return hip_fail(e, "k_ring");
-        }
-    }
-    if (aux) {  // the caller's stream continues once the dense groups are verified too
-        PIPCK_HIP(hipEventRecord(aux->join, aux->s));
-        PIPCK_HIP(hipStreamWaitEvent(s, aux->join, 0));
-    }
+    PIPCK_LAUNCHED("k_ring");
     return PIPCK_OK;
 }
 

@@ -86,12 +86,9 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
  * 0 switches every probe off. */
 void pipck_tune_probes(uint32_t probes);
 
-/* The ring verifier's schedule (pipck_rx_verify_ring; process-wide, internal,
- * every setting gives the same verdicts): 0 = automatic -- k_ring, and for slot
- * strides from 4 KiB its dense slot groups verified by k_ring_deep on a second
- * stream at the same time.  Bit 0 = k_ring's row stream never deals items
- * round-robin to the block's waves, bit 1 = always; bit 2 = no dense-group
- * split (k_ring alone, the round-5 default); bit 3 = the split at every stride. */
+/* k_ring's schedule switches (pipck_rx_verify_ring; process-wide, internal,
+ * every setting gives the same verdicts; 0 = automatic): bit 0 = its row stream
+ * never deals items round-robin to the block's waves, bit 1 = always. */
 void pipck_tune_ring(uint32_t mode);
 
 /* XCD-weighted static deal for k_flat (ring 24, checksum; measurement arm,

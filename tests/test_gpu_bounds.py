@@ -119,7 +119,7 @@ def _ipv4_frame(oracle, rng, l4len, k, total_override=None):
     return bytes(p)
 
 
-@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots", "deep", "nodeep"])
+@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots"])
 @pytest.mark.parametrize("stride", [1024, 9216])
 def test_ring_length_past_the_slot_is_an_error_not_a_fault(oracle, schedule, stride):
     """pipck_rx_verify_ring_n through ctypes, no Python guard, on a ring hipMalloc'd

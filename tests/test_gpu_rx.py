@@ -442,10 +442,8 @@ def _ring(frames, stride):
 # pipck_rx_verify_ring's three schedules (pipck_rxdev.hip): the default slot
 # groups (k_ring), the row stream (k_ring_rx, tune flag bit 28) and slot by slot
 # (k_ring_slots, the wave-per-packet arm)
-# (plus, from 4 KiB slots, k_ring_deep on a second stream for the dense slot
-# groups; "nodeep" = k_ring alone, "deep" = that split at every stride)
 RING_KERNELS = {"groups": "k_ring<8, 12>", "own": "k_ring<8, 12>", "coop": "k_ring<8, 12>", "rows": "k_ring_rx",
-                "slots": "k_ring_slots", "deep": "k_ring<8, 12>", "nodeep": "k_ring<8, 12>"}
+                "slots": "k_ring_slots"}
 
 
 def _ring_schedule(name):
@@ -459,10 +457,6 @@ def _ring_schedule(name):
         engine.tune(ring_own_slots=True)
     elif name == "coop":  # k_ring's row stream: items dealt round-robin to the block's waves
         engine.tune(ring_all_coop=True)
-    elif name == "deep":  # dense slot groups to k_ring_deep at every stride
-        engine.tune(ring_deep=True)
-    elif name == "nodeep":  # k_ring alone (the round-5 default)
-        engine.tune(ring_deep=False)
     else:
         engine.tune()
 
@@ -501,7 +495,7 @@ def _host_bits(frames):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("fill", ["mixed", "short", "dense"])
-@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots", "deep", "nodeep"])
+@pytest.mark.parametrize("schedule", ["groups", "own", "coop", "rows", "slots"])
 @pytest.mark.parametrize("stride", [1024, 2048, 9216])
 def test_rx_verify_ring_equals_host_path(oracle, stride, schedule, fill):
     """pipck_rx_verify_ring (frames in fixed-size slots of a device ring, the unused

@@ -41,8 +41,16 @@ def main() -> None:
     md = [f"# {tag}: RX verifier PMC passes (tools/pmc_rx.sh)", "",
           "HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), per dispatch of the RX kernel; "
           "algorithmic = frame bytes read + 1 verdict byte per frame (tools/rx_device_bench.py).", "",
-          "| workload | kernel | frames | algorithmic B | HBM B (PMC) | ratio | rocprof median ms | frac of 8 TB/s |",
-          "|---|---|---|---|---|---|---|---|"]
+          "Expected = the line model of tools/ring_expected_lines.py (profiles/r06_ring_expected_lines.jsonl): "
+          "every 128-B line a frame touches, fetched whole, + 2 B of slot length + the 1-B verdict per slot "
+          "(rings only; the byte-packed frames share lines with their neighbours).", "",
+          "| workload | kernel | frames | algorithmic B | HBM B (PMC) | ratio | expected lines/frame | expected ratio "
+          "| measured / expected | rocprof median ms | frac of 8 TB/s |",
+          "|---|---|---|---|---|---|---|---|---|---|---|"]
+    exp = {}
+    ef = ROOT / "profiles" / "r06_ring_expected_lines.jsonl"
+    if ef.exists():
+        exp = {d["what"]: d for d in map(json.loads, ef.read_text().splitlines())}
     for d in sorted((ROOT / "gpurun_out").glob(f"pmc_rx_{tag}_*")):
         wl = d.name[len(f"pmc_rx_{tag}_"):]
         lines = [json.loads(x) for x in (d / "trace.jsonl").read_text().splitlines() if x.startswith("{")]
@@ -68,10 +76,17 @@ def main() -> None:
              "traffic_over_algorithmic": round(hbm / algo, 4), "rocprof_dispatches": len(durs),
              "rocprof_median_ns": med, "frac_by_rocprof": round(algo / (med / 1e9) / 8e12, 4),
              "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts 1/2 of wide streams)"}
+        e = exp.get(wl)
+        if e and e["frames"] == line["packets"]:
+            t["expected_lines_per_frame"] = e["lines_per_frame"]
+            t["expected_ratio"] = e["expected_ratio"]
+            ecols = f"{e['lines_per_frame']:.3f} | {e['expected_ratio']:.4f} | {hbm / algo / e['expected_ratio']:.4f}"
+        else:
+            ecols = "- | - | -"
+        md.append(f"| {wl} | `{kname}` | {line['packets']:,} | {algo:,} | {int(hbm):,} | {hbm / algo:.4f} | "
+                  f"{ecols} | {med / 1e6:.4f} | {t['frac_by_rocprof']:.3f} |")
         (ROOT / "profiles" / f"traffic_rx_{wl if wl != 'packed' else 'rx_verify_device'}.json").write_text(
             json.dumps(t, indent=1) + "\n")
-        md.append(f"| {wl} | `{kname}` | {line['packets']:,} | {algo:,} | {int(hbm):,} | {hbm / algo:.3f} | "
-                  f"{med / 1e6:.4f} | {t['frac_by_rocprof']:.3f} |")
     md += ["", f"libpipck.so sha256 `{sha}`", ""]
     (ROOT / "profiles" / f"{tag}_rx_pmc_summary.md").write_text("\n".join(md))
     print("\n".join(md))

@@ -11,6 +11,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   tail -1 gpurun_out/pytest_ring.log
 fi
 timeout -k 10 500 python3 -u tools/rx_device_bench.py --skip-packed ${RINGS:+--rings $RINGS} ${ARMS:+--arms $ARMS} \
+  ${TUNES:+--tunes "$(cat $TUNES)"} \
   > gpurun_out/${TAG:-r06_ring}.jsonl 2> gpurun_out/${TAG:-r06_ring}.err || { tail -20 gpurun_out/${TAG:-r06_ring}.err; exit 1; }
 python3 -c "
 import json
