@@ -464,7 +464,7 @@ def _ring_schedule(name):
 def _ring_frames(oracle, rng, stride, fill, count):
     """count oracle-checksummed IPv4/IPv6 TCP/UDP/ICMP frames that fit the slot,
     every third damaged, some with link padding.  fill "mixed": L4 lengths up to
-    the slot; "dense": within ~200 B of filling the slot (k_ring_deep's groups),
+    the slot; "dense": within ~200 B of filling the slot (k_ring's interleaved row stream),
     with a run of short frames every 512; "short": frames in runs of 16 whose longest is <= 128 / 256 / 512
     bytes or up to the slot, so k_ring's waves take every schedule (S = 8, 16, 32
     lanes per slot, and the row stream)."""

@@ -1,7 +1,6 @@
 #!/bin/bash
-# Round 6: the ring verifier's dense-group split (k_ring + k_ring_deep): ring
-# parity tests, then the five bench rings under the default, k_ring alone, the
-# row stream and slot by slot (tools/rx_device_bench.py), one box.
+# Round 6: ring parity tests, then the bench rings (tools/rx_device_bench.py)
+# under the schedules named in $ARMS, one box.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out

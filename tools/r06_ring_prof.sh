@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of the ring bench (default arm) on the rings in $RINGS:
-# per-kernel durations of k_ring and k_ring_deep (they overlap on two streams).
+# per-kernel durations.
 set -u
 R="${GRAFT_REPO_ROOT:-$PWD}"
 mkdir -p "$R/gpurun_out"
