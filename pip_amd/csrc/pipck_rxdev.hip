@@ -36,6 +36,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 namespace pipck {
 
@@ -67,9 +69,47 @@ constexpr int kRingU = 24;
 
 __host__ __device__ constexpr uint32_t ring_pitch(uint32_t k) { return k | 1u; }
 
+// ---- the schedule's feedback (jumbo slots: k_ring or the row stream) --------
+// k_ring keeps 8 waves per SIMD, which sparse and short rings need; full jumbo
+// slots stream 3 % faster through the row stream at 3 waves per SIMD
+// (DESIGN.md section 9 f2), and a kernel's register budget is fixed at launch
+// while a ring's fill is not.  A ring buffer is verified again and again, so
+// each launch reports how full it was and the next launches of the same ring
+// take the schedule that fits: one block in kFbEvery evaluates ring_dense on
+// its slots and adds it to a device counter; the last to arrive writes
+// {seq, dense, reporting blocks} into pinned host memory, where launch_ring_rx
+// reads it for the following calls.  Speed only: both kernels give the same
+// verdicts, and a report that two overlapping calls mixed only mixes the
+// heuristic.
+constexpr uint32_t kFbEvery = 64;
+struct RingFb {
+    unsigned long long* ctr;  // device: (dense << 32) | arrived; the last to arrive resets it
+    uint32_t* host;           // pinned, coherent: {seq, dense, reported}
+    uint32_t parts;           // reporting blocks in this launch (blockIdx % kFbEvery == 0)
+    uint32_t seq;
+};
+// 64 slots are dense when the 1 KiB rows holding frame bytes (T) are at least
+// 3/4 of the rows of their slots -- full jumbo slots
+__device__ __forceinline__ bool ring_dense(uint32_t T, uint32_t nb, uint32_t stride) {
+    return 4u * T >= 3u * nb * ((stride + 1023u) >> 10);
+}
+// lane 0 of one wave of a reporting block: count its verdict, and the last
+// reporter publishes the launch's total (vector atomics and stores only)
+__device__ __forceinline__ void ring_report(const RingFb& fb, bool dense, int lane) {
+    if (lane != 0) return;
+    const unsigned long long old = atomicAdd(fb.ctr, ((unsigned long long)(dense ? 1u : 0u) << 32) | 1ull);
+    if ((uint32_t)old + 1u >= fb.parts) {  // the last reporter (or a count an overlapping call left)
+        atomicExch(fb.ctr, 0ull);
+        __hip_atomic_store(fb.host + 1, (uint32_t)(old >> 32) + (dense ? 1u : 0u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(fb.host + 2, (uint32_t)old + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(fb.host, fb.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_ring_rx(
     const uint8_t* __restrict__ arena, uint32_t cpp, const uint16_t* __restrict__ lens, uint64_t n, uint32_t K,
-    uint8_t* __restrict__ ok, uint32_t* __restrict__ err) {
+    uint8_t* __restrict__ ok, uint32_t* __restrict__ err, RingFb fb) {
     extern __shared__ uint32_t s_ring[];  // part[64][pitch] | len[K] | hdr[6][K] (u32x4), launch_ring_rx sizes it
     const uint32_t pitch = ring_pitch(K);
     uint32_t* s_part = s_ring;
@@ -166,6 +206,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         const bool bad = (uint32_t)lens[p0 + i] > 16u * cpp;
         if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
         store_result8(buf_rsrc(ok + p0, np), i, bad ? 0u : rx_from_window(pkp, L, F, hw));
+    }
+    // the feedback (launch_ring_rx passes it for jumbo slots only, where K <= 64)
+    if (fb.ctr && blockIdx.x % kFbEvery == 0 && w == 0) {
+        const uint32_t Ls = (uint32_t)lane < np ? s_len[lane] : 0u;  // refused slots: 0
+        ring_report(fb, ring_dense(wave_total((Ls + 1023u) >> 10), np, 16u * cpp), lane);
     }
 }
 
@@ -270,6 +315,9 @@ constexpr uint32_t kRingCoopRows = 2;  // mean rows per slot from which the wave
 // small kernel's depth and the result-store policy)
 constexpr uint32_t kRingOwnSlots = 1u;  // the row stream never interleaves its waves
 constexpr uint32_t kRingAllCoop = 2u;   // the row stream always interleaves them
+constexpr uint32_t kRingNoAdapt = 4u;   // no feedback: k_ring at every fill (the round-5 default)
+constexpr uint32_t kRingAdaptAll = 8u;  // the feedback at every slot stride (tests; default from 4 KiB)
+constexpr uint64_t kAdaptMinStride = 4096;  // jumbo slots: below, k_ring wins at every fill
 std::atomic<uint32_t> g_ring_mode{0};
 
 struct RingLds {
@@ -392,7 +440,7 @@ template <int U, int UD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ring(const uint8_t* __restrict__ arena, uint32_t stride,
                                               const uint16_t* __restrict__ lens, uint64_t n, uint32_t G,
                                               uint8_t* __restrict__ ok, uint32_t* __restrict__ err,
-                                              uint32_t kflags) {
+                                              uint32_t kflags, RingFb fb) {
     // (the block size is a compile-time constant: as a kernel argument it cost
     // the short-frame stream 40 %, profiles/r05_ring_schedule_ab.jsonl)
     constexpr uint32_t B = kRingB;
@@ -452,6 +500,77 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ri
     }
     if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
     store_result8(buf_rsrc(ok + b0, nb), (uint32_t)lane, r);
+    if (fb.ctr && blockIdx.x % kFbEvery == 0)  // the schedule's feedback (wave 0, after its stores)
+        ring_report(fb, ring_dense(wave_total((nch + 63u) >> 6), nb, stride), lane);
+}
+
+// Per-ring feedback state (host side of RingFb), keyed by (device, ring
+// address, slot stride); at most kFbRings rings, the least recently used one's
+// buffers reused for a new ring (a launch of the old ring still in flight can
+// then only mix the heuristic).  Never freed: 64 x (8 B device + 16 B pinned).
+struct FbEntry {
+    int dev = -1;
+    const void* ring = nullptr;
+    uint64_t stride = 0;
+    unsigned long long* d_ctr = nullptr;
+    uint32_t* h = nullptr;
+    uint32_t seq = 0;
+    uint64_t used = 0;
+};
+constexpr size_t kFbRings = 64;
+static std::mutex g_fb_mu;
+static std::vector<FbEntry> g_fb;
+static uint64_t g_fb_clock = 0;
+
+// The entry of this ring (created or recycled on first use, its counter zeroed
+// on `s`), its next sequence number, and whether its last published report says
+// the row stream fits: >= 90 % of the reporting blocks found their slots dense.
+static int ring_feedback(const void* ring, uint64_t stride, hipStream_t s, RingFb* fb, bool* rows) {
+    int dev = 0;
+    PIPCK_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_fb_mu);
+    FbEntry* e = nullptr;
+    for (auto& x : g_fb)
+        if (x.dev == dev && x.ring == ring && x.stride == stride) e = &x;
+    if (!e) {
+        if (g_fb.size() < kFbRings) {
+            FbEntry x;
+            x.dev = dev;
+            PIPCK_HIP(hipMalloc(reinterpret_cast<void**>(&x.d_ctr), sizeof(unsigned long long)));
+            if (hipHostMalloc(reinterpret_cast<void**>(&x.h), 4 * sizeof(uint32_t), hipHostMallocCoherent) !=
+                hipSuccess) {
+                (void)hipFree(x.d_ctr);
+                set_error("pipck_rx_verify_ring: hipHostMalloc of the feedback word failed");
+                return PIPCK_ENOMEM;
+            }
+            g_fb.push_back(x);
+            e = &g_fb.back();
+        } else {
+            e = &g_fb[0];
+            for (auto& x : g_fb)
+                if (x.dev == dev && x.used < e->used) e = &x;
+            if (e->dev != dev) {  // every entry belongs to other devices: no feedback this call
+                fb->ctr = nullptr;
+                *rows = false;
+                return PIPCK_OK;
+            }
+        }
+        e->ring = ring;
+        e->stride = stride;
+        e->seq = 0;
+        __atomic_store_n(&e->h[0], 0u, __ATOMIC_RELAXED);
+        PIPCK_HIP(hipMemsetAsync(e->d_ctr, 0, sizeof(unsigned long long), s));
+    }
+    e->used = ++g_fb_clock;
+    if (++e->seq == 0) e->seq = 1;
+    const uint32_t seen = __atomic_load_n(&e->h[0], __ATOMIC_ACQUIRE);
+    const uint32_t dense = __atomic_load_n(&e->h[1], __ATOMIC_RELAXED);
+    const uint32_t parts = __atomic_load_n(&e->h[2], __ATOMIC_RELAXED);
+    *rows = seen != 0 && parts != 0 && 10ull * dense >= 9ull * parts;
+    fb->ctr = e->d_ctr;
+    fb->host = e->h;
+    fb->seq = e->seq;
+    return PIPCK_OK;
 }
 
 int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens, uint64_t n, uint8_t* d_ok,
@@ -468,6 +587,15 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     }
     const uint32_t cpp = (uint32_t)(stride / 16);
     const uint32_t flags = g_ring_mode.load();
+    // jumbo slots: k_ring or the row stream, by the feedback of this ring's
+    // earlier launches (speed only, the verdicts are the same)
+    RingFb fb{nullptr, nullptr, 0u, 0u};
+    bool rows = false;
+    if (!wave_arm() && !alt_schedule() && !(flags & kRingNoAdapt) &&
+        (stride >= kAdaptMinStride || (flags & kRingAdaptAll))) {
+        const int rc = ring_feedback(d_arena, stride, s, &fb, &rows);
+        if (rc) return rc;
+    }
     if (wave_arm()) {  // measurement arm: slot by slot, a wave per slot
         const uint64_t blocks = (n + 4u * kSlotG - 1) / (4u * kSlotG);
         if (blocks > 0x7FFFFFFFull) {
@@ -479,7 +607,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         PIPCK_LAUNCHED("k_ring_slots");
         return PIPCK_OK;
     }
-    if (alt_schedule()) {  // measurement arm: the row stream over whole slots
+    if (alt_schedule() || rows) {  // the row stream over whole slots (dense jumbo rings; tune bit 28: always)
         // K slots per block task: ~4 waves x 48 rows (x 64 for jumbo slots), a
         // multiple of 8, at most 256 (one slot per thread at the end) -- k_flat_coop's
         uint32_t K = (4u * (cpp >= 256 ? 64u : 48u) * 64u) / cpp;
@@ -491,8 +619,12 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
             return PIPCK_ERANGE;
         }
         const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
+        if (fb.ctr) {
+            if (K > 64) fb.ctr = nullptr;  // a report reads one wave's lengths: tasks of <= 64 slots only
+            fb.parts = (uint32_t)((blocks + kFbEvery - 1) / kFbEvery);
+        }
         PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
-                     d_ok, d_err);
+                     d_ok, d_err, fb);
         PIPCK_LAUNCHED("k_ring_rx");
         return PIPCK_OK;
     }
@@ -515,11 +647,12 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     }
     const uint8_t* a = (const uint8_t*)d_arena;
     const uint32_t st = (uint32_t)stride;
+    fb.parts = (uint32_t)((blocks + kFbEvery - 1) / kFbEvery);
     // loads in flight per wave: U in the short and own-slot streams, UD in the
     // interleaved one (loads_per_lane 16 / 24: both; 17 / 25: UD only)
 #define PIPCK_RING(UU, UUD)                                                                                     \
     PIPCK_LAUNCH((k_ring<UU, UUD>), dim3((uint32_t)blocks), dim3(256), 0, s, a, st, d_lens, n, G, d_ok, d_err,    \
-                 flags)
+                 flags, fb)
     switch (g_tune_loads()) {
         case 8: PIPCK_RING(8, 8); break;
         case 12: PIPCK_RING(12, 12); break;

@@ -86,9 +86,13 @@ void pipck_tune(uint32_t lanes_per_packet, uint32_t loads_per_lane, uint32_t blo
  * 0 switches every probe off. */
 void pipck_tune_probes(uint32_t probes);
 
-/* k_ring's schedule switches (pipck_rx_verify_ring; process-wide, internal,
- * every setting gives the same verdicts; 0 = automatic): bit 0 = its row stream
- * never deals items round-robin to the block's waves, bit 1 = always. */
+/* The ring verifier's schedule switches (pipck_rx_verify_ring; process-wide,
+ * internal, every setting gives the same verdicts; 0 = automatic: k_ring, and
+ * for slot strides from 4 KiB k_ring or the row stream k_ring_rx as the
+ * feedback of the same ring's earlier launches says it is full): bit 0 =
+ * k_ring's row stream never deals items round-robin to the block's waves,
+ * bit 1 = always; bit 2 = no feedback (k_ring at every fill, the round-5
+ * default); bit 3 = the feedback at every stride. */
 void pipck_tune_ring(uint32_t mode);
 
 /* XCD-weighted static deal for k_flat (ring 24, checksum; measurement arm,

@@ -579,15 +579,17 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
          end_no_store: bool = False, alt_flat_schedule: bool = False,
          plain_result_stores: bool = False, wave_stores: bool = False, free_run: bool = False,
          packed_no_align: bool = False, hdr_in_place: bool = False, ring_own_slots: bool = False,
-         ring_all_coop: bool = False) -> None:
+         ring_all_coop: bool = False, ring_adapt: bool | None = None) -> None:
     """Process-wide launch-shape override (0 = automatic) for tests and tools: the internal pipck_tune
     (pip_amd/csrc/pipck_testing.h), not part of the public ABI.  Every setting computes the same results
     except the measurement-only probes loads_only (bit 21), no_task_end (22), end_no_store (23) and
     hdr_in_place (pipck_tune_probes bit 0, not a tune flag: k_hdr stores the results into the headers'
     ip_sum and leaves the result array untouched).  alt_flat_schedule (bit 28) never changes results.
     ring_own_slots / ring_all_coop: k_ring's row stream never / always deals items round-robin to the
-    block's waves -- pipck_tune_ring's own word, apart from the flags above (they once
-    shared bits 27 / 29 with small_k_log and plain_result_stores)."""
+    block's waves; ring_adapt: None = automatic (jumbo slots take k_ring or the row stream by the
+    feedback of the ring's earlier launches), False = k_ring at every fill, True = the feedback at every
+    stride -- pipck_tune_ring's own word, apart from the flags above (they once shared bits
+    27 / 29 with small_k_log and plain_result_stores)."""
     if not 0 <= small_k_log <= 4:
         raise ValueError("small_k_log must be 0..4")
     flags = ((1 if plain_loads else 0) | (0 if flat else 2) | (4 if nt_loads else 0) | (8 if xcd_groups else 0)
@@ -601,4 +603,5 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
     load().pipck_tune_probes(1 if hdr_in_place else 0)
-    load().pipck_tune_ring((1 if ring_own_slots else 0) | (2 if ring_all_coop else 0))
+    load().pipck_tune_ring((1 if ring_own_slots else 0) | (2 if ring_all_coop else 0)
+                           | {None: 0, False: 4, True: 8}[ring_adapt])

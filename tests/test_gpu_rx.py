@@ -457,8 +457,8 @@ def _ring_schedule(name):
         engine.tune(ring_own_slots=True)
     elif name == "coop":  # k_ring's row stream: items dealt round-robin to the block's waves
         engine.tune(ring_all_coop=True)
-    else:
-        engine.tune()
+    else:  # "groups": k_ring itself, whatever the ring's earlier launches reported
+        engine.tune(ring_adapt=False)
 
 
 def _ring_frames(oracle, rng, stride, fill, count):
@@ -600,7 +600,10 @@ def test_rx_verify_ring_default_schedule(oracle, stride):
         frames.append(bytes(p))
     ring, lens = _ring(frames, stride)
     dev = engine.rx_verify_ring(ring, stride, lens).cpu().numpy()
-    assert RING_KERNELS["groups"] in _last_kernel()
+    # the first launch on a ring is k_ring; from 4 KiB slots a later one may take
+    # the row stream when this address's earlier launches (another test's ring
+    # at a reused address) reported full slots
+    assert RING_KERNELS["groups"] in _last_kernel() or (stride >= 4096 and "k_ring_rx" in _last_kernel())
     for schedule in ("own", "coop", "rows", "slots"):
         _ring_schedule(schedule)
         try:
@@ -610,3 +613,52 @@ def test_rx_verify_ring_default_schedule(oracle, stride):
             engine.tune()
         assert np.array_equal(dev, other), schedule
     assert 600 < int((dev == VERIFIED).sum()) < 700
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [4096, 9216])
+def test_rx_verify_ring_adapts_to_the_fill(stride):
+    """The default schedule of jumbo-slot rings follows the ring's own fill: a ring
+    of full slots starts on k_ring and, once a launch has reported its fill (a
+    synchronise in between), takes the row stream k_ring_rx; when the same ring
+    (same address) then holds short frames, it goes back to k_ring.  Every launch
+    gives the verdicts k_ring gives (tune ring_adapt=False) on the same bytes."""
+    import torch
+
+    from pip_amd import engine
+
+    n = 64 * 1000 + 37
+    engine.tune()
+    try:
+        ring, lens, _ = engine.gen_rx_ring(n, 17, stride, l4_len=stride - 300)
+        engine.tune(ring_adapt=False)
+        want = engine.rx_verify_ring(ring, stride, lens).clone()
+        assert "k_ring<8, 12>" in _last_kernel()
+        engine.tune()
+        kernels = []
+        for _ in range(6):
+            got = engine.rx_verify_ring(ring, stride, lens)
+            kernels.append(_last_kernel())
+            torch.cuda.synchronize()
+            assert torch.equal(got, want)
+        assert "k_ring_rx" in kernels[-1], kernels
+        # the same ring now holds short frames only: back to k_ring
+        short = torch.minimum(lens.to(torch.int32) & 0xFFFF, torch.tensor(300, device=lens.device)).to(torch.int16)
+        engine.tune(ring_adapt=False)
+        want2 = engine.rx_verify_ring(ring, stride, short).clone()
+        engine.tune()
+        kernels = []
+        for _ in range(6):
+            got = engine.rx_verify_ring(ring, stride, short)
+            kernels.append(_last_kernel())
+            torch.cuda.synchronize()
+            assert torch.equal(got, want2)
+        assert "k_ring<8, 12>" in kernels[-1], kernels
+        # a sparse ring (Zipf frames in 9 KiB slots, 220-B frames in 4 KiB) never leaves k_ring
+        ring3, lens3, _ = engine.gen_rx_ring(n, 19, stride, l4_len=0 if stride >= 9216 else 200)
+        for _ in range(4):
+            engine.rx_verify_ring(ring3, stride, lens3)
+            torch.cuda.synchronize()
+            assert "k_ring<8, 12>" in _last_kernel()
+    finally:
+        engine.tune()

@@ -55,7 +55,7 @@ def main():
     ap.add_argument("--rings", default="ring_sparse_9216,ring_dense_1536,ring_dense_9216,ring_short_2048,ring_short_1024")
     ap.add_argument("--tune", default="{}", help="engine.tune kwargs for the packed arms and the default (groups) ring arm, JSON")
     ap.add_argument("--skip-packed", action="store_true", help="rings only")
-    ap.add_argument("--arms", default="groups,rows,slots",
+    ap.add_argument("--arms", default="groups,kring,rows,slots",
                     help="ring schedules to time; groups:NAME = the default with --tunes[NAME]")
     ap.add_argument("--tunes", default="{}", help='JSON {"NAME": engine.tune kwargs} for groups:NAME arms')
     a = ap.parse_args()
@@ -129,6 +129,8 @@ def main():
                     engine.tune(lanes_per_packet=256)
                 elif arm == "rows":
                     engine.tune(alt_flat_schedule=True)
+                elif arm == "kring":  # k_ring at every fill (no feedback)
+                    engine.tune(**{**tune_default, "ring_adapt": False})
                 elif arm.startswith("groups:"):
                     engine.tune(**tunes[arm.split(":", 1)[1]])
                 else:
