@@ -481,7 +481,12 @@ int pipck_rx_verify_device(const void* d_arena, uint64_t arena_bytes, const uint
  * slot with d_lens[i] > slot_stride (a corrupt or foreign length) is not read
  * at all -- no load and no header parse leaves its slot -- gets d_ok[i] = 0,
  * and d_err (optional, device u32) gets (1 << PIPCK_ERANGE).  One kernel on
- * `stream`, asynchronous; d_ok[i] as pipck_rx_verify_device. */
+ * `stream`, asynchronous; d_ok[i] as pipck_rx_verify_device.  For slot strides
+ * from 4 KiB the kernel's schedule follows the fill this ring (d_arena,
+ * slot_stride) reported in earlier calls -- a row stream for full slots,
+ * slot groups otherwise; the verdicts are the same either way.  The first call
+ * on a ring allocates 8 bytes of device and 16 of pinned host memory that stay
+ * with the library (at most 64 rings remembered). */
 int pipck_rx_verify_ring_n(const void* d_arena, uint64_t slot_stride, const uint16_t* d_lens, uint64_t n_slots,
                            uint8_t* d_ok, uint32_t* d_err, void* stream);
 /* pipck_rx_verify_ring_n without the error word (slots are bounded the same way). */

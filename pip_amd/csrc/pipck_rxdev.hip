@@ -75,19 +75,25 @@ __host__ __device__ constexpr uint32_t ring_pitch(uint32_t k) { return k | 1u; }
 // (DESIGN.md section 9 f2), and a kernel's register budget is fixed at launch
 // while a ring's fill is not.  A ring buffer is verified again and again, so
 // each launch reports how full it was and the next launches of the same ring
-// take the schedule that fits: one block in kFbEvery evaluates ring_dense on
-// its slots and adds it to a device counter; the last to arrive writes
+// take the schedule that fits: a sample of the blocks evaluates ring_dense on
+// its slots and adds it to a device counter (every-th block: ~64 reporters per
+// launch, spread over the ring); the last to arrive writes
 // {seq, dense, reporting blocks} into pinned host memory, where launch_ring_rx
 // reads it for the following calls.  Speed only: both kernels give the same
 // verdicts, and a report that two overlapping calls mixed only mixes the
 // heuristic.
-constexpr uint32_t kFbEvery = 64;
+constexpr uint32_t kFbReports = 64;  // reporting blocks per launch (at most)
 struct RingFb {
     unsigned long long* ctr;  // device: (dense << 32) | arrived; the last to arrive resets it
     uint32_t* host;           // pinned, coherent: {seq, dense, reported}
-    uint32_t parts;           // reporting blocks in this launch (blockIdx % kFbEvery == 0)
+    uint32_t every;           // blocks with blockIdx % every == 0 report
+    uint32_t parts;           // reporting blocks in this launch
     uint32_t seq;
 };
+static inline void fb_sample(RingFb& fb, uint64_t blocks) {
+    fb.every = (uint32_t)std::max<uint64_t>(1, blocks / kFbReports);
+    fb.parts = (uint32_t)((blocks + fb.every - 1) / fb.every);
+}
 // 64 slots are dense when the 1 KiB rows holding frame bytes (T) are at least
 // 3/4 of the rows of their slots -- full jumbo slots
 __device__ __forceinline__ bool ring_dense(uint32_t T, uint32_t nb, uint32_t stride) {
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         store_result8(buf_rsrc(ok + p0, np), i, bad ? 0u : rx_from_window(pkp, L, F, hw));
     }
     // the feedback (launch_ring_rx passes it for jumbo slots only, where K <= 64)
-    if (fb.ctr && blockIdx.x % kFbEvery == 0 && w == 0) {
+    if (fb.ctr && blockIdx.x % fb.every == 0 && w == 0) {
         const uint32_t Ls = (uint32_t)lane < np ? s_len[lane] : 0u;  // refused slots: 0
         ring_report(fb, ring_dense(wave_total((Ls + 1023u) >> 10), np, 16u * cpp), lane);
     }
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80))) void k_ri
     }
     if (bad && err) atomicOr(err, 1u << PIPCK_ERANGE);
     store_result8(buf_rsrc(ok + b0, nb), (uint32_t)lane, r);
-    if (fb.ctr && blockIdx.x % kFbEvery == 0)  // the schedule's feedback (wave 0, after its stores)
+    if (fb.ctr && blockIdx.x % fb.every == 0)  // the schedule's feedback (wave 0, after its stores)
         ring_report(fb, ring_dense(wave_total((nch + 63u) >> 6), nb, stride), lane);
 }
 
@@ -589,10 +595,14 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     const uint32_t flags = g_ring_mode.load();
     // jumbo slots: k_ring or the row stream, by the feedback of this ring's
     // earlier launches (speed only, the verdicts are the same)
-    RingFb fb{nullptr, nullptr, 0u, 0u};
+    RingFb fb{nullptr, nullptr, 1u, 0u, 0u};
     bool rows = false;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (!wave_arm() && !alt_schedule() && !(flags & kRingNoAdapt) &&
-        (stride >= kAdaptMinStride || (flags & kRingAdaptAll))) {
+        (stride >= kAdaptMinStride || (flags & kRingAdaptAll)) &&
+        hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+        // (a stream being captured into a graph gets k_ring: the feedback's first
+        // use allocates, and a replayed launch would keep reporting one sequence)
         const int rc = ring_feedback(d_arena, stride, s, &fb, &rows);
         if (rc) return rc;
     }
@@ -621,7 +631,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
         const size_t lds = 4u * (64u * ring_pitch(K) + ((K + 3u) & ~3u)) + 16u * 6u * K;
         if (fb.ctr) {
             if (K > 64) fb.ctr = nullptr;  // a report reads one wave's lengths: tasks of <= 64 slots only
-            fb.parts = (uint32_t)((blocks + kFbEvery - 1) / kFbEvery);
+            fb_sample(fb, blocks);
         }
         PIPCK_LAUNCH(k_ring_rx, dim3((uint32_t)blocks), dim3(256), lds, s, (const uint8_t*)d_arena, cpp, d_lens, n, K,
                      d_ok, d_err, fb);
@@ -647,7 +657,7 @@ int launch_ring_rx(const void* d_arena, uint64_t stride, const uint16_t* d_lens,
     }
     const uint8_t* a = (const uint8_t*)d_arena;
     const uint32_t st = (uint32_t)stride;
-    fb.parts = (uint32_t)((blocks + kFbEvery - 1) / kFbEvery);
+    fb_sample(fb, blocks);
     // loads in flight per wave: U in the short and own-slot streams, UD in the
     // interleaved one (loads_per_lane 16 / 24: both; 17 / 25: UD only)
 #define PIPCK_RING(UU, UUD)                                                                                     \

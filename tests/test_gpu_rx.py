@@ -454,9 +454,9 @@ def _ring_schedule(name):
     elif name == "slots":
         engine.tune(lanes_per_packet=256)
     elif name == "own":  # k_ring's row stream: each wave its own 16 slots
-        engine.tune(ring_own_slots=True)
+        engine.tune(ring_own_slots=True, ring_adapt=False)
     elif name == "coop":  # k_ring's row stream: items dealt round-robin to the block's waves
-        engine.tune(ring_all_coop=True)
+        engine.tune(ring_all_coop=True, ring_adapt=False)
     else:  # "groups": k_ring itself, whatever the ring's earlier launches reported
         engine.tune(ring_adapt=False)
 
