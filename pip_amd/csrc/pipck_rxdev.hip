@@ -538,28 +538,31 @@ static int ring_feedback(const void* ring, uint64_t stride, hipStream_t s, RingF
     FbEntry* e = nullptr;
     for (auto& x : g_fb)
         if (x.dev == dev && x.ring == ring && x.stride == stride) e = &x;
+    fb->ctr = nullptr;  // no feedback unless an entry is found or made below (then k_ring)
+    *rows = false;
     if (!e) {
+        FbEntry x;
+        x.dev = dev;
+        bool made = false;
         if (g_fb.size() < kFbRings) {
-            FbEntry x;
-            x.dev = dev;
-            PIPCK_HIP(hipMalloc(reinterpret_cast<void**>(&x.d_ctr), sizeof(unsigned long long)));
-            if (hipHostMalloc(reinterpret_cast<void**>(&x.h), 4 * sizeof(uint32_t), hipHostMallocCoherent) !=
-                hipSuccess) {
+            if (hipMalloc(reinterpret_cast<void**>(&x.d_ctr), sizeof(unsigned long long)) != hipSuccess) {
+                (void)hipGetLastError();  // (our own failure) recycle an entry instead
+            } else if (hipHostMalloc(reinterpret_cast<void**>(&x.h), 4 * sizeof(uint32_t), hipHostMallocCoherent) !=
+                       hipSuccess) {
+                (void)hipGetLastError();
                 (void)hipFree(x.d_ctr);
-                set_error("pipck_rx_verify_ring: hipHostMalloc of the feedback word failed");
-                return PIPCK_ENOMEM;
+            } else {
+                made = true;
             }
+        }
+        if (made) {
+            if (g_fb.empty()) g_fb.reserve(kFbRings);
             g_fb.push_back(x);
             e = &g_fb.back();
         } else {
-            e = &g_fb[0];
-            for (auto& x : g_fb)
-                if (x.dev == dev && x.used < e->used) e = &x;
-            if (e->dev != dev) {  // every entry belongs to other devices: no feedback this call
-                fb->ctr = nullptr;
-                *rows = false;
-                return PIPCK_OK;
-            }
+            for (auto& y : g_fb)  // recycle this device's least recently used ring
+                if (y.dev == dev && (!e || y.used < e->used)) e = &y;
+            if (!e) return PIPCK_OK;  // every entry belongs to other devices
         }
         e->ring = ring;
         e->stride = stride;

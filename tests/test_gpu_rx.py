@@ -662,3 +662,30 @@ def test_rx_verify_ring_adapts_to_the_fill(stride):
             assert "k_ring<8, 12>" in _last_kernel()
     finally:
         engine.tune()
+
+
+@pytest.mark.gpu
+def test_rx_verify_ring_feedback_recycles_entries():
+    """More jumbo-slot rings than the feedback remembers (64): the least recently
+    used entries are recycled, and every call still gives k_ring's verdicts --
+    full rings and sparse ones interleaved at distinct addresses."""
+    import torch
+
+    from pip_amd import engine
+
+    stride, n = 4096, 64 * 3 + 5
+    rings = []
+    for k in range(70):
+        ring, lens, _ = engine.gen_rx_ring(n, 100 + k, stride, l4_len=stride - 300 if k % 2 else 200)
+        engine.tune(ring_adapt=False)
+        want = engine.rx_verify_ring(ring, stride, lens).clone()
+        engine.tune()
+        rings.append((ring, lens, want))
+    try:
+        for _ in range(3):
+            for ring, lens, want in rings:
+                got = engine.rx_verify_ring(ring, stride, lens)
+                torch.cuda.synchronize()
+                assert torch.equal(got, want)
+    finally:
+        engine.tune()
