@@ -497,18 +497,18 @@ def mem_available() -> int:
 
 def host_bytes_per_packet(w) -> int:
     """Host memory the CPU legs hold per sampled packet: the packet bytes (a fixed
-    slot, or cfg4's Zipf mean rounded up generously), the pip_buf chain copy the
-    chain leg builds, results and per-packet metadata."""
-    per = w.stride if not w.ragged else 1024
-    return 2 * per + 64
+    slot, or cfg4's Zipf mean of ~990 B rounded up), plus the chain leg's two
+    pip_buf objects (they point into the same bytes, ref_chains_build), results
+    and per-packet metadata."""
+    return (w.stride if not w.ragged else 1024) + 256
 
 
 def sample_that_fits(n: int, per_packet: int) -> int:
-    """n, or the largest sample whose host footprint fits a quarter of MemAvailable."""
+    """n, or the largest sample whose host footprint fits half of MemAvailable."""
     avail = mem_available()
-    if not avail or n * per_packet <= avail // 4:
+    if not avail or n * per_packet <= avail // 2:
         return n
-    return max(1 << 12, int(avail // 4 // per_packet))
+    return max(1 << 12, int(avail // 2 // per_packet))
 
 
 def cpu_legs(args, w, gpu_out, count, first, dev=None):
@@ -531,7 +531,7 @@ def cpu_legs(args, w, gpu_out, count, first, dev=None):
     # the sample BASELINE.md ("Which inputs") prescribes: the full batch for cfg1-cfg4,
     # the first 1M packets for cfg5 (64M x 8,980 B cannot be host-resident) -- up to
     # ~9 GB of host memory (cfg3, cfg5); --cpu-sample overrides it.  A host with too
-    # little free memory for that gets the largest sample that fits in a quarter of
+    # little free memory for that gets the largest sample that fits in half of
     # what is available, and the line's "sample" says so.
     plan = f"BASELINE.md plan: {'first 1M packets of the per-GPU shard' if w.cfg == 5 else 'the full batch'}"
     n_plan = args.cpu_sample or min(count, 1 << 20 if w.cfg == 5 else count)

@@ -182,3 +182,21 @@ def test_injected_start_skew_lowers_the_aggregate(tmp_path, capfd, world):
     assert skewed["span_s"] > skewed["max_rank_s"] + 0.1
     assert skewed["rate"] < 0.75 * skewed["rate_max_rank"]
     assert skewed["rate"] == pytest.approx(world * 1e9 * 5 / skewed["span_s"])
+
+
+def test_cpu_sample_falls_back_to_the_memory_the_host_has(monkeypatch):
+    """the CPU baseline's BASELINE.md sample (up to ~9 GB) is cut to
+    what half of MemAvailable holds, never below 4K packets; the full plan when it
+    fits or when /proc/meminfo cannot be read."""
+    from pip_amd.workloads import BY_CFG
+
+    w = BY_CFG[5]
+    per = bench.host_bytes_per_packet(w)
+    assert per >= w.stride
+    monkeypatch.setattr(bench, "mem_available", lambda: 64 << 30)
+    assert bench.sample_that_fits(1 << 20, per) == 1 << 20
+    monkeypatch.setattr(bench, "mem_available", lambda: 4 << 30)
+    n = bench.sample_that_fits(1 << 20, per)
+    assert 4096 <= n < 1 << 20 and n * per <= 2 << 30
+    monkeypatch.setattr(bench, "mem_available", lambda: 0)
+    assert bench.sample_that_fits(1 << 20, per) == 1 << 20
