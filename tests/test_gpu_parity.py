@@ -1233,6 +1233,41 @@ def test_full_size_fixed(oracle, w, n, first):
     torch.cuda.empty_cache()
 
 
+def test_cfg5_full_shard_bit_exact_with_pip():
+    """The headline shard in bulk: all 8M cfg5 packets of
+    rank 1's shard (ids 8M..16M, 75 GB) checksummed on the GPU by the bench kernel,
+    then every result compared with pip's own compiled pip_inet_checksum
+    (oracle/_ref; the oracle's restatement where _ref is absent) over the same
+    bytes, regenerated on the host in 512K-packet chunks -- not a sample."""
+    import os
+
+    from oracle.oracle import Oracle, Reference
+
+    w, n, first = CFG5, 8 << 20, 8 << 20
+    arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
+    engine.gen_fixed(arena, w.stride, w.length, n, first, w.seed, w.hdr)
+    out = engine.checksum_fixed(arena, w.stride, w.length, n, _pseudo(w), N_FLOWS, None, first)
+    assert "k_flat_coop<32," in last_kernel()
+    got = u16(out)
+    del arena, out
+    torch.cuda.empty_cache()
+    orc = Oracle()
+    ref = Reference() if Reference.available() else None
+    flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    chunk = 1 << 19
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        host = orc.gen_fixed_batch(w.seed, first + c0, m, w.length, w.hdr, w.stride, threads)
+        if ref is not None:
+            want = ref.batch_fixed(host, w.stride, w.length, m, w.family, w.proto, flows, N_FLOWS, first + c0, threads)
+        else:
+            want = orc.batch_fixed(host, w.stride, w.length, m, w.family, w.proto, w.seed, N_FLOWS, first + c0, threads)
+        bad = np.nonzero(got[c0:c0 + m] != want)[0]
+        assert bad.size == 0, (c0, bad[:5])
+        del host
+
+
 def test_full_size_ragged(oracle):
     w, n = CFG4, 8 << 20
     arena, desc, lens = engine.gen_ragged(n, 0, w.seed, w.hdr, N_FLOWS)
