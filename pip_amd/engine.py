@@ -603,5 +603,6 @@ def tune(lanes_per_packet: int = 0, loads_per_lane: int = 0, blocks: int = 0, pl
              | (1 << 31 if free_run else 0))
     load().pipck_tune(lanes_per_packet, loads_per_lane, blocks, flags)
     load().pipck_tune_probes(1 if hdr_in_place else 0)
-    load().pipck_tune_ring((1 if ring_own_slots else 0) | (2 if ring_all_coop else 0)
-                           | {None: 0, False: 4, True: 8}[ring_adapt])
+    ring = (1 if ring_own_slots else 0) | (2 if ring_all_coop else 0) | {None: 0, False: 4, True: 8}[ring_adapt]
+    if ring or hasattr(load(), "pipck_tune_ring"):  # (a pre-1.3 build under PIPCK_LIB has no ring word)
+        load().pipck_tune_ring(ring)
