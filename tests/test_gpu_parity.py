@@ -1233,17 +1233,21 @@ def test_full_size_fixed(oracle, w, n, first):
     torch.cuda.empty_cache()
 
 
-def test_cfg5_full_shard_bit_exact_with_pip():
-    """The headline shard in bulk: all 8M cfg5 packets of
-    rank 1's shard (ids 8M..16M, 75 GB) checksummed on the GPU by the bench kernel,
-    then every result compared with pip's own compiled pip_inet_checksum
-    (oracle/_ref; the oracle's restatement where _ref is absent) over the same
-    bytes, regenerated on the host in 512K-packet chunks -- not a sample."""
+BULK = [(CFG2, 4 << 20, 0), (CFG3, 1 << 20, 0), (CFG5, 8 << 20, 8 << 20)]
+
+
+@pytest.mark.parametrize("w,n,first", BULK, ids=[w.name for w, _, _ in BULK])
+def test_full_batch_bit_exact_with_pip(w, n, first):
+    """Each fixed-stride BASELINE batch in bulk: every packet
+    -- cfg5's 8M of rank 1's shard (ids 8M..16M, 75 GB), cfg2's 4M, cfg3's 1M --
+    checksummed on the GPU by the bench kernel, then every result compared with
+    pip's own compiled pip_inet{,6}_checksum (oracle/_ref; the oracle's
+    restatement where _ref is absent) over the same bytes, regenerated on the
+    host in 512K-packet chunks -- not a sample."""
     import os
 
     from oracle.oracle import Oracle, Reference
 
-    w, n, first = CFG5, 8 << 20, 8 << 20
     arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
     engine.gen_fixed(arena, w.stride, w.length, n, first, w.seed, w.hdr)
     out = engine.checksum_fixed(arena, w.stride, w.length, n, _pseudo(w), N_FLOWS, None, first)
@@ -1266,6 +1270,46 @@ def test_cfg5_full_shard_bit_exact_with_pip():
         bad = np.nonzero(got[c0:c0 + m] != want)[0]
         assert bad.size == 0, (c0, bad[:5])
         del host
+
+
+def test_cfg4_full_batch_bit_exact_with_pip():
+    """cfg4 in bulk, byte-packed as the bench runs it: all 8M Zipf packets
+    checksummed by the bench kernel (k_packedb), then the arena's own bytes copied
+    back in ~1M-packet pieces and every packet checksummed by pip's compiled
+    pip_inet_checksum (oracle/_ref; the restatement where it is absent) at its
+    byte offset -- not a sample."""
+    import os
+
+    from oracle.oracle import Oracle, Reference
+
+    w, n = CFG4, 8 << 20
+    arena, lens16, to, lens = engine.gen_packed_bytes(n, 0, w.seed, w.hdr)
+    _, pseudo = engine.gen_flows(4, N_FLOWS, w.seed, w.proto)
+    out = engine.checksum_packed_bytes(arena, lens16, to, n, pseudo, N_FLOWS, None, 0)
+    assert "k_packedb<" in last_kernel()
+    got = u16(out)
+    L = lens.cpu().numpy().astype(np.uint32)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(L.astype(np.uint64))[:-1]
+    orc = Oracle()
+    ref = Reference() if Reference.available() else None
+    flows = orc.flows_table(4, w.seed, N_FLOWS, w.proto)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    chunk = 1 << 20
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        b0, b1 = int(offs[c0]), int(offs[c0 + m - 1]) + int(L[c0 + m - 1])
+        host = arena[b0:b1].cpu().numpy()
+        o = offs[c0:c0 + m] - np.uint64(b0)
+        if ref is not None:
+            want = ref.batch_ragged(host, o, L[c0:c0 + m], 4, w.proto, flows, N_FLOWS, c0, threads)
+        else:
+            want = orc.batch_ragged(host, o, L[c0:c0 + m], 4, w.proto, w.seed, N_FLOWS, c0, threads)
+        bad = np.nonzero(got[c0:c0 + m] != want)[0]
+        assert bad.size == 0, (c0, bad[:5])
+        del host
+    del arena, out
+    torch.cuda.empty_cache()
 
 
 def test_full_size_ragged(oracle):
