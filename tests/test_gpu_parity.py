@@ -1233,17 +1233,19 @@ def test_full_size_fixed(oracle, w, n, first):
     torch.cuda.empty_cache()
 
 
-BULK = [(CFG2, 4 << 20, 0), (CFG3, 1 << 20, 0), (CFG5, 8 << 20, 8 << 20)]
+BULK = [(CFG1, 1 << 20, 0, "k_small<"), (CFG1, 256 << 20, 3, "k_hdr<5,"), (CFG2, 4 << 20, 0, "k_flat_coop<32,"),
+        (CFG3, 1 << 20, 0, "k_flat_coop<32,"), (CFG5, 8 << 20, 8 << 20, "k_flat_coop<32,")]
 
 
-@pytest.mark.parametrize("w,n,first", BULK, ids=[w.name for w, _, _ in BULK])
-def test_full_batch_bit_exact_with_pip(w, n, first):
+@pytest.mark.parametrize("w,n,first,kernel", BULK, ids=[f"{w.name}_{n}" for w, n, _, _ in BULK])
+def test_full_batch_bit_exact_with_pip(w, n, first, kernel):
     """Each fixed-stride BASELINE batch in bulk: every packet
-    -- cfg5's 8M of rank 1's shard (ids 8M..16M, 75 GB), cfg2's 4M, cfg3's 1M --
-    checksummed on the GPU by the bench kernel, then every result compared with
-    pip's own compiled pip_inet{,6}_checksum (oracle/_ref; the oracle's
+    -- cfg5's 8M of rank 1's shard (ids 8M..16M, 75 GB), cfg2's 4M, cfg3's 1M,
+    cfg1's 1M headers and 256M (f3's size) -- checksummed on the GPU by the
+    bench kernel, then every result compared with pip's own compiled
+    pip_inet{,6}_checksum / pip_ip_checksum (oracle/_ref; the oracle's
     restatement where _ref is absent) over the same bytes, regenerated on the
-    host in 512K-packet chunks -- not a sample."""
+    host in chunks -- not a sample."""
     import os
 
     from oracle.oracle import Oracle, Reference
@@ -1251,7 +1253,7 @@ def test_full_batch_bit_exact_with_pip(w, n, first):
     arena = torch.empty(n * w.stride, dtype=torch.uint8, device=DEV)
     engine.gen_fixed(arena, w.stride, w.length, n, first, w.seed, w.hdr)
     out = engine.checksum_fixed(arena, w.stride, w.length, n, _pseudo(w), N_FLOWS, None, first)
-    assert "k_flat_coop<32," in last_kernel()
+    assert kernel in last_kernel()
     got = u16(out)
     del arena, out
     torch.cuda.empty_cache()
@@ -1259,7 +1261,7 @@ def test_full_batch_bit_exact_with_pip(w, n, first):
     ref = Reference() if Reference.available() else None
     flows = orc.flows_table(w.family, w.seed, N_FLOWS, w.proto)
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    chunk = 1 << 19
+    chunk = max(1 << 19, n >> 5)
     for c0 in range(0, n, chunk):
         m = min(chunk, n - c0)
         host = orc.gen_fixed_batch(w.seed, first + c0, m, w.length, w.hdr, w.stride, threads)
