@@ -3,6 +3,9 @@
 # round-5 build (pip_amd/lib/ab/libpipck_r05.so, PIPCK_LIB) on one box,
 # processes alternating r05 / r06 twice ("no slower than
 # r05"). Output: gpurun_out/ring_vs_r05_<build>_<pass>.jsonl
+# The round-5 library is git-ignored; rebuild it (sha256 2288e7e3...) with
+#   d=$(mktemp -d) && git archive 5b004ec | tar -x -C $d && make -C $d/pip_amd lib/libpipck.so \
+#     && mkdir -p pip_amd/lib/ab && cp $d/pip_amd/lib/libpipck.so pip_amd/lib/ab/libpipck_r05.so
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
