@@ -654,12 +654,20 @@ def test_rx_verify_ring_adapts_to_the_fill(stride):
             torch.cuda.synchronize()
             assert torch.equal(got, want2)
         assert "k_ring<8, 12>" in kernels[-1], kernels
-        # a sparse ring (Zipf frames in 9 KiB slots, 220-B frames in 4 KiB) never leaves k_ring
+        # a sparse ring (Zipf frames in 9 KiB slots, 220-B frames in 4 KiB) stays on
+        # k_ring once it has reported (its first launch may follow an earlier
+        # test's dense ring freed at the same address), verdicts unchanged
         ring3, lens3, _ = engine.gen_rx_ring(n, 19, stride, l4_len=0 if stride >= 9216 else 200)
+        engine.tune(ring_adapt=False)
+        want3 = engine.rx_verify_ring(ring3, stride, lens3).clone()
+        engine.tune()
+        kernels = []
         for _ in range(4):
-            engine.rx_verify_ring(ring3, stride, lens3)
+            got = engine.rx_verify_ring(ring3, stride, lens3)
+            kernels.append(_last_kernel())
             torch.cuda.synchronize()
-            assert "k_ring<8, 12>" in _last_kernel()
+            assert torch.equal(got, want3)
+        assert all("k_ring<8, 12>" in k for k in kernels[1:]), kernels
     finally:
         engine.tune()
 
